@@ -1,0 +1,279 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident rx parse + checksum + classify throughput on MI355X.
+
+Workload (BASELINE.json configs[2], "C3"): 2^20 x 1500 B synthetic Eth/IPv4/TCP frames per
+GPU, 1 000 flows + 1 listener, records of 16 B, inputs resident in HBM before timing.  One
+step = one rxg_rx_burst_dev over the whole batch.  A 64 B leg (configs[1], "C2") is reported
+beside it with a rotating 1 GiB working set (16 copies of 2^20 frames) so the 256 MiB
+Infinity Cache cannot hold it.
+
+Multi-GPU: one process per GPU (torch.distributed.run), weak scaling, every rank its own
+shard (seed + rank) and a replica of the TCB mirror; no data-path collective.  The only
+collective is the RCCL all-reduce that merges the per-GPU counters.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import rxg  # noqa: E402  (after torch: one HIP runtime per process)
+
+METRIC = "Mpps + GB/s rx parse+checksum+classify, device-resident, 64B & 1500B frames"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+WORKLOADS = {
+    # name: (frame_len, flows, mix, rotating copies)
+    "c3_1500B_1Kflows": (1500, 1000, 0, 1),
+    "c2_64B_1flow": (64, 1, 0, 16),
+    "c4_imix_64Kflows": (0, 65536, 1, 3),
+}
+
+
+# --------------------------------------------------------------- distributed helpers ---
+def rank_env():
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def shard_seed(base: int, rank: int) -> int:
+    """Weak scaling: rank r generates its own independent batch."""
+    return (base * 1_000_003 + rank * 7919 + 1) & 0xFFFFFFFFFFFF
+
+
+def merge_counters(counters: np.ndarray, device) -> np.ndarray:
+    """Sum the per-GPU counters over ranks (RCCL all-reduce on GPU, gloo on CPU)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return counters.copy()
+    t = torch.from_numpy(counters.astype(np.int64)).to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy().astype(np.uint64)
+
+
+def max_over_ranks(x: float, device) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(device):
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+
+
+# ------------------------------------------------------------------------ workload ---
+class Workload:
+    """`copies` independent synthetic batches of n frames resident in HBM."""
+
+    def __init__(self, eng, name, n, seed, rec=rxg.REC16):
+        self.name, self.n, self.rec = name, n, rec
+        self.frame_len, self.flows, self.mix, self.copies = WORKLOADS[name]
+        self.batches = []
+        for c in range(self.copies):
+            self.batches.append(eng.synth(n=n, nflows=self.flows, len_a=self.frame_len or 1500,
+                                          mix=self.mix, seed=seed + 17 * c))
+        eng.sync()
+        self.lens = self.batches[0]["len"].download(np.uint16, n)
+        self.bytes_per_batch = int(self.lens.astype(np.uint64).sum())
+        self.out = eng.alloc(n * rec)
+
+    def launch(self, eng, i, stream=None):
+        b = self.batches[i % self.copies]
+        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, self.n, self.out.ptr,
+                         self.rec, stream)
+
+    def free(self):
+        for b in self.batches:
+            for v in b.values():
+                if isinstance(v, rxg.DevArray):
+                    v.free()
+        self.out.free()
+
+
+def time_workload(eng, wl, steps, warmup, device, stream):
+    for i in range(warmup):
+        wl.launch(eng, i, stream)
+    eng.sync()
+    eng.counters_reset()
+    evs = [(eng.event(), eng.event()) for _ in range(steps)]
+    barrier(device)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        eng.record(evs[i][0], stream)
+        wl.launch(eng, warmup + i, stream)
+        eng.record(evs[i][1], stream)
+    eng.sync()
+    barrier(device)
+    elapsed = time.perf_counter() - t0
+    kern_ms = [eng.elapsed_ms(a, b) for a, b in evs]
+    return elapsed, kern_ms
+
+
+def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
+    """The oracle's faithful restatement of the reference rx path (port), on one host
+    core, over a bounded sample of the same workload (first sample_n frames)."""
+    import oracle
+    b = wl.batches[0]
+    n = min(sample_n, wl.n)
+    off = b["off64"].download(np.uint32, n)
+    lens = b["len"].download(np.uint16, n)
+    end = int(off[-1]) * 64 + int(lens[-1])
+    arena = b["arena"].download(np.uint8, (end + 63) // 64 * 64)
+    tcb, live = rxg.synthetic_tcb_table(wl.flows)
+    res = {}
+    for opt, budget in (("O0", seconds * 0.5), ("O2", seconds * 0.5)):
+        oracle.arp_reset()
+        oracle.rx_batch(arena, off, lens, tcb, live, faithful=True, opt=opt)  # learn ARP
+        pk = by = 0
+        t0 = time.perf_counter()
+        chunk = max(64, min(n, 2000))
+        s = 0
+        while time.perf_counter() - t0 < budget:
+            e = min(s + chunk, n)
+            oracle.rx_batch(arena, off[s:e], lens[s:e], tcb, live, faithful=True, opt=opt)
+            pk += e - s
+            by += int(lens[s:e].astype(np.uint64).sum())
+            s = 0 if e >= n else e
+        dt = time.perf_counter() - t0
+        res[opt] = (pk / dt / 1e6, by / dt / 1e9, pk, dt)
+    oracle.arp_reset()
+    mpps0, gbs0, pk0, dt0 = res["O0"]
+    mpps2, gbs2, pk2, dt2 = res["O2"]
+    return {"value": round(gbs0, 6), "unit": "GB/s", "mpps": round(mpps0, 6), "cores": 1,
+            "kind": "port",
+            "sample": (f"faithful oracle (reference algorithms: byte-loop checksum, malloc+memcpy "
+                       f"pseudo header, two-pass linear findtcb over {wl.flows + 1} TCBs, ARP list "
+                       f"walks, disabled-logger calls) built -O0 like tcp_ip_stack/Makefile:50, "
+                       f"{pk0} frames of this workload in {dt0:.1f} s on 1 core; "
+                       f"-O2 build: {mpps2:.4f} Mpps / {gbs2:.4f} GB/s"),
+            "o2": {"mpps": round(mpps2, 6), "gbs": round(gbs2, 6)}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c3_1500B_1Kflows", choices=sorted(WORKLOADS))
+    ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU per step")
+    ap.add_argument("--rec", type=int, default=16, choices=[16, 48])
+    ap.add_argument("--no-legs", action="store_true", help="skip the 64 B / IMIX legs")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    rank, world, local = rank_env()
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(local)
+    eng = rxg.Engine(device=local)
+    stream = None  # the engine's own stream
+
+    seed = shard_seed(0x5EED0001, rank)
+    wl = Workload(eng, args.workload, args.frames, seed, args.rec)
+    tcb, live = rxg.synthetic_tcb_table(wl.flows)
+    eng.tcb_load(tcb, live)
+    eng.tcb_sync()
+
+    elapsed, kern_ms = time_workload(eng, wl, args.steps, args.warmup, device, stream)
+    cnt = eng.counters()
+    elapsed_max = max_over_ranks(elapsed, device)
+    merged = merge_counters(cnt, device)
+
+    total_frames = wl.n * args.steps * world
+    total_bytes = wl.bytes_per_batch * args.steps * world
+    gbs = total_bytes / elapsed_max / 1e9
+    mpps = total_frames / elapsed_max / 1e6
+    k_avg_s = float(np.mean(kern_ms)) / 1e3
+    achieved = wl.bytes_per_batch / k_avg_s / 1e9
+    C = {name: int(merged[i]) for i, name in enumerate(rxg.COUNTERS)}
+    checks_ok = (C["rx"] == total_frames and C["bytes"] == total_bytes
+                 and C["ip_cksum_bad"] == 0 and C["tcp_cksum_bad"] == 0
+                 and C["dispatch"] == total_frames and C["tcb_hit_exact"] == total_frames)
+
+    legs = {}
+    if not args.no_legs:
+        for name in ("c2_64B_1flow", "c4_imix_64Kflows"):
+            if name == args.workload:
+                continue
+            lw = Workload(eng, name, args.frames, seed + 99, args.rec)
+            t2, l2 = rxg.synthetic_tcb_table(lw.flows)
+            eng.tcb_load(t2, l2)
+            e2, k2 = time_workload(eng, lw, args.steps, args.warmup, device, stream)
+            e2 = max_over_ranks(e2, device)
+            c2 = merge_counters(eng.counters(), device)
+            ka = float(np.mean(k2)) / 1e3
+            legs[name] = {
+                "mpps": round(lw.n * args.steps * world / e2 / 1e6, 2),
+                "gbs": round(lw.bytes_per_batch * args.steps * world / e2 / 1e9, 2),
+                "kernel_us": round(ka * 1e6, 2),
+                "roofline_frac": round(lw.bytes_per_batch / ka / 1e9 / HBM_PEAK_GBS, 4),
+                "working_set_GiB": round(lw.copies * (lw.batches[0]["arena_bytes"]) / 2**30, 3),
+                "counters_ok": bool(int(c2[0]) == lw.n * args.steps * world
+                                    and int(c2[7]) == 0 and int(c2[8]) == 0),
+            }
+            lw.free()
+        eng.tcb_load(tcb, live)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(gbs, 2),
+            "unit": "GB/s",
+            "mpps": round(mpps, 2),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device-generated Eth/IPv4/TCP frames, valid checksums, "
+                    "SURVEY.md 8(d))",
+            "config": {"workload": args.workload, "frames_per_gpu": wl.n,
+                       "frame_len": wl.frame_len or "imix", "flows": wl.flows,
+                       "tcbs": wl.flows + 1, "record_bytes": args.rec,
+                       "bytes_per_gpu_step": wl.bytes_per_batch,
+                       "parallelism": f"dp{world} (independent batches, replicated TCB mirror)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None,
+                         "kernel_us": round(k_avg_s * 1e6, 2),
+                         "algorithmic_bytes_per_launch": wl.bytes_per_batch},
+            "cpu_baseline": cpu,
+            "counters_ok": bool(checks_ok),
+            "counters": C,
+            "legs": legs,
+            "build": rxg.load_library().rxg_build_info().decode(),
+        }
+        print(json.dumps(line), flush=True)
+
+    wl.free()
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,635 @@
+// rxg_host.cpp — host side of the rxg C ABI (include/rxg.h).
+//
+// Owns one GPU context: its stream, the device TCB mirror (rebuilt from the host mirror
+// whenever a rxg_tcb_* call made it dirty), the counter block, and the pinned staging used
+// by the host-buffer entry points.  There is no CPU compute path: without a usable HIP
+// device every compute entry point returns -ENODEV / -EIO.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "rxg.h"
+#include "rxg_common.h"
+#include "rxg_kernels.h"
+
+using namespace rxg;
+
+static_assert(sizeof(rxg_rec16) == 16, "rxg_rec16 layout");
+static_assert(sizeof(rxg_rec48) == 48, "rxg_rec48 layout");
+static_assert(sizeof(rxg_tcb_tuple) == 20, "rxg_tcb_tuple layout");
+
+// ------------------------------------------------------------------------ errors ---
+static thread_local char g_err[512];
+
+static int fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_OK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(-EIO, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,      \
+                        __LINE__);                                                          \
+    } while (0)
+
+extern "C" const char *rxg_last_error(void) { return g_err; }
+
+// ---------------------------------------------------------------------- context ---
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct rxg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t max_blocks = 2048;
+
+    // host mirror of tcbs[0..ntcb)
+    std::vector<rxg_tcb_tuple> tcb;
+    std::vector<uint8_t> live;
+    bool dirty = true;
+
+    // device mirror
+    DevBuf buckets, listen, state;
+    uint32_t bucket_mask = 0;
+    int32_t dev_ntcb = 0;
+    int32_t dev_min_null = INT32_MAX;
+
+    unsigned long long *counters = nullptr;
+
+    // host-buffer burst staging
+    uint32_t max_batch = 0;
+    uint64_t max_bytes = 0;
+    uint8_t *h_arena = nullptr;
+    uint32_t *h_off = nullptr;
+    uint16_t *h_len = nullptr;
+    uint8_t *d_arena = nullptr;
+    uint32_t *d_off = nullptr;
+    uint16_t *d_len = nullptr;
+    uint8_t *d_out = nullptr;
+};
+
+struct rxg_event {
+    hipEvent_t e;
+};
+
+static int set_device(rxg_ctx *c) { HIP_OK(hipSetDevice(c->device)); return 0; }
+
+static int ensure(DevBuf &b, size_t bytes)
+{
+    if (b.bytes >= bytes && b.p) return 0;
+    if (b.p) HIP_OK(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    HIP_OK(hipMalloc(&b.p, want));
+    b.bytes = want;
+    return 0;
+}
+
+extern "C" int rxg_abi_version(void) { return RXG_ABI_VERSION; }
+
+extern "C" const char *rxg_build_info(void)
+{
+    return "rxg " __DATE__ " gfx950"
+#if RXG_NT_LOADS
+           " nt-loads"
+#endif
+        ;
+}
+
+extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
+{
+    if (!out) return fail(-EINVAL, "rxg_init: out is NULL");
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0)
+        return fail(-ENODEV, "rxg_init: no HIP device (%s)", hipGetErrorString(e));
+    rxg_ctx *c = new rxg_ctx();
+    c->device = cfg ? cfg->device : 0;
+    if (c->device < 0 || c->device >= ndev) {
+        delete c;
+        return fail(-EINVAL, "rxg_init: device %d of %d", cfg ? cfg->device : 0, ndev);
+    }
+    int rc = set_device(c);
+    if (rc) { delete c; return rc; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) {
+        // persistent grid: 8 workgroups of 256 threads per CU
+        c->max_blocks = (uint32_t)prop.multiProcessorCount * 8u;
+        if (const char *g = getenv("RXG_MAX_BLOCKS")) c->max_blocks = (uint32_t)atoi(g);
+        if (c->max_blocks == 0) c->max_blocks = 2048;
+    }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(-EIO, "rxg_init: hipStreamCreate failed");
+    }
+    if (hipMalloc(&c->counters, RXG_NCOUNTERS * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->counters, 0, RXG_NCOUNTERS * sizeof(unsigned long long)) != hipSuccess) {
+        rxg_fini(c);
+        return fail(-ENOMEM, "rxg_init: counters");
+    }
+    c->max_batch = cfg ? cfg->max_batch : 0;
+    c->max_bytes = cfg ? cfg->max_bytes : 0;
+    if (c->max_batch) {
+        uint64_t ab = c->max_bytes ? c->max_bytes : (uint64_t)c->max_batch * 2048u;
+        c->max_bytes = ab;
+        if (hipHostMalloc((void **)&c->h_arena, ab, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_off, c->max_batch * 4u, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_len, c->max_batch * 2u, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(&c->d_arena, ab) != hipSuccess ||
+            hipMalloc(&c->d_off, c->max_batch * 4u) != hipSuccess ||
+            hipMalloc(&c->d_len, c->max_batch * 2u) != hipSuccess ||
+            hipMalloc(&c->d_out, (size_t)c->max_batch * 48u) != hipSuccess) {
+            rxg_fini(c);
+            return fail(-ENOMEM, "rxg_init: staging for %u frames / %llu bytes", c->max_batch,
+                        (unsigned long long)ab);
+        }
+    }
+    *out = c;
+    return 0;
+}
+
+extern "C" int rxg_fini(rxg_ctx *c)
+{
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf *b : {&c->buckets, &c->listen, &c->state})
+        if (b->p) (void)hipFree(b->p);
+    if (c->counters) (void)hipFree(c->counters);
+    if (c->h_arena) (void)hipHostFree(c->h_arena);
+    if (c->h_off) (void)hipHostFree(c->h_off);
+    if (c->h_len) (void)hipHostFree(c->h_len);
+    if (c->d_arena) (void)hipFree(c->d_arena);
+    if (c->d_off) (void)hipFree(c->d_off);
+    if (c->d_len) (void)hipFree(c->d_len);
+    if (c->d_out) (void)hipFree(c->d_out);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+extern "C" int rxg_sync(rxg_ctx *c)
+{
+    if (!c) return fail(-EINVAL, "rxg_sync: ctx NULL");
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" void *rxg_stream(rxg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+static hipStream_t pick(rxg_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+
+// -------------------------------------------------------------------- TCB mirror ---
+static int grow_to(rxg_ctx *c, int32_t idx)
+{
+    if (idx < 0) return fail(-EINVAL, "tcb index %d < 0", idx);
+    if ((size_t)idx >= c->tcb.size()) {
+        c->tcb.resize((size_t)idx + 1, rxg_tcb_tuple{});
+        c->live.resize((size_t)idx + 1, 0);
+    }
+    return 0;
+}
+
+extern "C" int rxg_tcb_upsert(rxg_ctx *c, int32_t idx, const rxg_tcb_tuple *t)
+{
+    if (!c || !t) return fail(-EINVAL, "rxg_tcb_upsert: NULL argument");
+    int rc = grow_to(c, idx);
+    if (rc) return rc;
+    c->tcb[idx] = *t;
+    c->live[idx] = 1;
+    c->dirty = true;
+    return 0;
+}
+
+extern "C" int rxg_tcb_remove(rxg_ctx *c, int32_t idx)
+{
+    if (!c) return fail(-EINVAL, "rxg_tcb_remove: ctx NULL");
+    if (idx < 0 || (size_t)idx >= c->tcb.size())
+        return fail(-EINVAL, "rxg_tcb_remove: index %d outside Ntcb %zu", idx, c->tcb.size());
+    c->live[idx] = 0;
+    c->dirty = true;
+    return 0;
+}
+
+extern "C" int rxg_tcb_set_state(rxg_ctx *c, int32_t idx, uint8_t state)
+{
+    if (!c) return fail(-EINVAL, "rxg_tcb_set_state: ctx NULL");
+    if (idx < 0 || (size_t)idx >= c->tcb.size() || !c->live[idx])
+        return fail(-EINVAL, "rxg_tcb_set_state: index %d is not a live slot", idx);
+    c->tcb[idx].state = state;
+    c->dirty = true;
+    return 0;
+}
+
+extern "C" int rxg_tcb_load(rxg_ctx *c, const rxg_tcb_tuple *tcbs, const uint8_t *live, int32_t ntcb)
+{
+    if (!c || ntcb < 0 || (ntcb > 0 && !tcbs)) return fail(-EINVAL, "rxg_tcb_load: bad arguments");
+    c->tcb.assign(tcbs, tcbs + ntcb);
+    if (live)
+        c->live.assign(live, live + ntcb);
+    else
+        c->live.assign((size_t)ntcb, 1);
+    c->dirty = true;
+    return 0;
+}
+
+extern "C" int32_t rxg_tcb_count(rxg_ctx *c) { return c ? (int32_t)c->tcb.size() : -EINVAL; }
+
+static inline bool port_ok(int32_t p) { return p >= 0 && p <= 0xFFFF; }
+
+// Rebuild the device mirror from the host mirror (DESIGN.md §TCB mirror).
+extern "C" int rxg_tcb_sync(rxg_ctx *c)
+{
+    if (!c) return fail(-EINVAL, "rxg_tcb_sync: ctx NULL");
+    if (!c->dirty) return 0;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const int32_t n = (int32_t)c->tcb.size();
+
+    // exact tuples -> lowest index (pass 1 returns the first live match)
+    struct Key {
+        uint32_t ports, dst, src;
+        bool operator==(const Key &o) const { return ports == o.ports && dst == o.dst && src == o.src; }
+    };
+    struct KeyHash {
+        size_t operator()(const Key &k) const { return tuple_hash(k.ports, k.dst, k.src); }
+    };
+    std::unordered_map<Key, int32_t, KeyHash> first;
+    first.reserve((size_t)n * 2 + 1);
+    std::vector<int32_t> listen(65536, -1);
+    std::vector<uint8_t> state((size_t)std::max(n, 1), RXG_STATE_NONE);
+    int32_t min_null = INT32_MAX;
+    for (int32_t i = 0; i < n; ++i) {
+        if (!c->live[i]) {
+            if (min_null == INT32_MAX) min_null = i;
+            continue;
+        }
+        const rxg_tcb_tuple &t = c->tcb[i];
+        state[i] = t.state;
+        // a tuple whose int ports are outside 0..65535 can never equal a packet's u16 port
+        if (port_ok(t.dport) && port_ok(t.sport)) {
+            Key k{((uint32_t)t.dport << 16) | (uint32_t)t.sport, t.ipv4_dst, t.ipv4_src};
+            first.emplace(k, i);  // keeps the lowest index
+        }
+        if (t.state == RXG_LISTENING && port_ok(t.dport) && listen[t.dport] < 0) listen[t.dport] = i;
+    }
+    // buckets: load factor <= 1/2 of the slots
+    uint32_t nb = 1;
+    while ((uint64_t)nb * kSlotsPerBucket < (uint64_t)first.size() * 2u) nb <<= 1;
+    std::vector<uint32_t> slots((size_t)nb * kSlotsPerBucket * 4u, 0u);
+    for (size_t s = 0; s < (size_t)nb * kSlotsPerBucket; ++s) slots[s * 4 + 3] = kEmpty;
+    for (const auto &kv : first) {
+        uint32_t b = tuple_hash(kv.first.ports, kv.first.dst, kv.first.src) & (nb - 1);
+        for (;;) {
+            int placed = 0;
+            for (int s = 0; s < kSlotsPerBucket && !placed; ++s) {
+                uint32_t *e = &slots[((size_t)b * kSlotsPerBucket + s) * 4];
+                if (e[3] == kEmpty) {
+                    e[0] = kv.first.ports;
+                    e[1] = kv.first.dst;
+                    e[2] = kv.first.src;
+                    e[3] = (uint32_t)kv.second;
+                    placed = 1;
+                }
+            }
+            if (placed) break;
+            b = (b + 1) & (nb - 1);
+        }
+    }
+    if ((rc = ensure(c->buckets, slots.size() * 4))) return rc;
+    if ((rc = ensure(c->listen, listen.size() * 4))) return rc;
+    if ((rc = ensure(c->state, state.size()))) return rc;
+    HIP_OK(hipMemcpyAsync(c->buckets.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->listen.p, listen.data(), listen.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->state.p, state.data(), state.size(), hipMemcpyHostToDevice, c->stream));
+    // the host vectors die here: the copies must have consumed them
+    HIP_OK(hipStreamSynchronize(c->stream));
+    c->bucket_mask = nb - 1;
+    c->dev_ntcb = n;
+    c->dev_min_null = min_null;
+    c->dirty = false;
+    return 0;
+}
+
+static DevTable table_view(const rxg_ctx *c)
+{
+    DevTable t;
+    t.buckets = (const uint4 *)c->buckets.p;
+    t.listen = (const int32_t *)c->listen.p;
+    t.state = (const uint8_t *)c->state.p;
+    t.bucket_mask = c->bucket_mask;
+    t.ntcb = c->dev_ntcb;
+    t.min_null = c->dev_min_null;
+    t.pad = 0;
+    return t;
+}
+
+// ------------------------------------------------------------------------- bursts ---
+extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream)
+{
+    if (!c || !b) return fail(-EINVAL, "rxg_rx_burst_dev: NULL argument");
+    if (b->rec_kind != RXG_REC16 && b->rec_kind != RXG_REC48)
+        return fail(-EINVAL, "rxg_rx_burst_dev: rec_kind %u", b->rec_kind);
+    if (b->n && (!b->frames || !b->off64 || !b->len || !b->out))
+        return fail(-EINVAL, "rxg_rx_burst_dev: NULL device pointer");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (c->dirty && (rc = rxg_tcb_sync(c))) return rc;
+    LaunchRx L;
+    L.frames = (const uint8_t *)b->frames;
+    L.off64 = b->off64;
+    L.len = b->len;
+    L.n = b->n;
+    L.mode = (int)b->rec_kind;
+    L.out = (uint8_t *)b->out;
+    L.table = table_view(c);
+    L.counters = c->counters;
+    L.max_blocks = c->max_blocks;
+    HIP_OK(launch_rx(L, pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *stream)
+{
+    if (!c || !b) return fail(-EINVAL, "rxg_tx_cksum_dev: NULL argument");
+    if (b->n && (!b->frames || !b->off64 || !b->len))
+        return fail(-EINVAL, "rxg_tx_cksum_dev: NULL device pointer");
+    int rc = set_device(c);
+    if (rc) return rc;
+    LaunchRx L;
+    std::memset(&L, 0, sizeof L);
+    L.frames = (const uint8_t *)b->frames;
+    L.off64 = b->off64;
+    L.len = b->len;
+    L.n = b->n;
+    L.mode = 0;
+    L.out = nullptr;
+    L.counters = nullptr;
+    L.max_blocks = c->max_blocks;
+    HIP_OK(launch_rx(L, pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, uint32_t rec_kind,
+                            void *out_host)
+{
+    if (!c || (n && (!pkts || !out_host))) return fail(-EINVAL, "rxg_rx_burst: NULL argument");
+    if (rec_kind != RXG_REC16 && rec_kind != RXG_REC48)
+        return fail(-EINVAL, "rxg_rx_burst: rec_kind %u", rec_kind);
+    if (n > c->max_batch)
+        return fail(-EINVAL, "rxg_rx_burst: n=%u exceeds max_batch=%u", n, c->max_batch);
+    int rc = set_device(c);
+    if (rc) return rc;
+    uint64_t slot = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t l = pkts[i].data_len;
+        const uint64_t need = (uint64_t)((l + 63u) / 64u);
+        if ((slot + need) * 64u > c->max_bytes)
+            return fail(-ENOMEM, "rxg_rx_burst: staging arena of %llu bytes is full at frame %u",
+                        (unsigned long long)c->max_bytes, i);
+        if (slot > UINT32_MAX) return fail(-ENOMEM, "rxg_rx_burst: arena offset overflow");
+        c->h_off[i] = (uint32_t)slot;
+        c->h_len[i] = (uint16_t)l;
+        if (l) std::memcpy(c->h_arena + slot * 64u, (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off, l);
+        slot += need;
+    }
+    if (n == 0) return 0;
+    HIP_OK(hipMemcpyAsync(c->d_arena, c->h_arena, slot * 64u, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->d_off, c->h_off, n * 4u, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->d_len, c->h_len, n * 2u, hipMemcpyHostToDevice, c->stream));
+    rxg_dev_batch b;
+    b.frames = c->d_arena;
+    b.off64 = c->d_off;
+    b.len = c->d_len;
+    b.n = n;
+    b.rec_kind = rec_kind;
+    b.out = c->d_out;
+    if ((rc = rxg_rx_burst_dev(c, &b, c->stream))) return rc;
+    HIP_OK(hipMemcpyAsync(out_host, c->d_out, (size_t)n * rec_kind, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ----------------------------------------------------------------------- counters ---
+extern "C" int rxg_counters_reset(rxg_ctx *c, void *stream)
+{
+    if (!c) return fail(-EINVAL, "rxg_counters_reset: ctx NULL");
+    HIP_OK(hipMemsetAsync(c->counters, 0, RXG_NCOUNTERS * sizeof(unsigned long long), pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
+{
+    if (!c || !out) return fail(-EINVAL, "rxg_counters_read: NULL argument");
+    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipMemcpy(out, c->counters, RXG_NCOUNTERS * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" void *rxg_counters_dev(rxg_ctx *c) { return c ? (void *)c->counters : nullptr; }
+
+// ------------------------------------------------------------------------- replay ---
+// The side effects of etherin.c:21-35, ip.c:26-39 and tcp_in.c:47-72, in packet order.
+extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const *mbufs,
+                             void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t stride)
+{
+    if (!c || !ops || (n && (!mbufs || !frames || !recs)))
+        return fail(-EINVAL, "rxg_rx_replay: NULL argument");
+    if (stride != RXG_REC16 && stride != RXG_REC48) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
+    for (uint32_t i = 0; i < n; ++i) {
+        const rxg_rec16 *r = (const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
+        void *m = mbufs[i];
+        uint8_t *f = (uint8_t *)frames[i];
+        void *ip = f + RXG_OFF_IP, *tcp = f + RXG_OFF_TCP;
+        switch (r->verdict) {
+        case RXG_V_ARP:
+            if (ops->arp_in) ops->arp_in(ops->user, m);
+            if (ops->free_mbuf) ops->free_mbuf(ops->user, m);
+            break;
+        case RXG_V_DROP_L2:
+        case RXG_V_DROP_NONTCP:
+            if (ops->free_mbuf) ops->free_mbuf(ops->user, m);
+            break;
+        default: {
+            // ip.c:30-32 ARP learn on the host-order source address
+            const uint32_t src = ((uint32_t)f[26] << 24) | ((uint32_t)f[27] << 16) | ((uint32_t)f[28] << 8) | f[29];
+            unsigned char mac[6];
+            if (ops->get_mac && ops->add_mac && ops->get_mac(ops->user, src, mac) == 0)
+                ops->add_mac(ops->user, src, f + 6);
+            if (r->verdict == RXG_V_RST_NOPCB || r->verdict == RXG_V_RST_LISTEN_NONSYN) {
+                if (ops->free_mbuf) ops->free_mbuf(ops->user, m);
+                if (ops->send_reset) ops->send_reset(ops->user, ip, tcp);
+            } else {  // RXG_V_DISPATCH
+                const uint32_t seq = ((uint32_t)f[38] << 24) | ((uint32_t)f[39] << 16) | ((uint32_t)f[40] << 8) | f[41];
+                const uint32_t ack = ((uint32_t)f[42] << 24) | ((uint32_t)f[43] << 16) | ((uint32_t)f[44] << 8) | f[45];
+                if (ops->on_segment) ops->on_segment(ops->user, r->tcb_idx, seq, ack);
+                if (ops->tcpswitch) ops->tcpswitch(ops->user, r->tcb_idx, r->state, tcp, ip, m);
+            }
+        }
+        }
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------- synthetic ---
+extern "C" uint64_t rxg_synth_arena_bytes(const rxg_synth_params *p)
+{
+    if (!p) return 0;
+    if (p->mix == 0) return (uint64_t)p->n * (uint64_t)((p->len_a + 63u) / 64u) * 64u;
+    return (uint64_t)((p->n + kImixBlock - 1) / kImixBlock) * kImixSlotsPerBlock * 64u;
+}
+
+extern "C" int rxg_synth_dev(rxg_ctx *c, const rxg_synth_params *p, void *frames, uint64_t cap,
+                             uint32_t *off64, uint16_t *len, uint32_t *flow_out, uint64_t *arena_bytes,
+                             void *stream)
+{
+    if (!c || !p || !frames || !off64 || !len) return fail(-EINVAL, "rxg_synth_dev: NULL argument");
+    if (p->mix > 1) return fail(-EINVAL, "rxg_synth_dev: mix %u", p->mix);
+    if (p->mix == 0 && (p->len_a < 54 || p->len_a > 9014))
+        return fail(-EINVAL, "rxg_synth_dev: len_a %u outside 54..9014", p->len_a);
+    const uint64_t need = rxg_synth_arena_bytes(p);
+    if (need > cap) return fail(-ENOMEM, "rxg_synth_dev: needs %llu arena bytes, have %llu",
+                                (unsigned long long)need, (unsigned long long)cap);
+    if (need / 64u > UINT32_MAX) return fail(-EINVAL, "rxg_synth_dev: arena beyond 256 GiB");
+    int rc = set_device(c);
+    if (rc) return rc;
+    hipStream_t st = pick(c, stream);
+    LaunchSynth L;
+    L.frames = (uint8_t *)frames;
+    L.off64 = off64;
+    L.len = len;
+    L.flow = flow_out;
+    L.seed = p->seed;
+    L.arena_bytes = need;
+    L.n = p->n;
+    L.nflows = p->nflows;
+    L.dst_ip = p->dst_ip_host;
+    L.dport = p->dport;
+    L.mix = p->mix;
+    L.len_a = p->len_a;
+    HIP_OK(launch_synth(L, st));
+    // checksums: the transmit generate kernel (ip_out's two checksums)
+    rxg_dev_tx_batch tb;
+    tb.frames = frames;
+    tb.off64 = off64;
+    tb.len = len;
+    tb.n = p->n;
+    tb.pad = 0;
+    if ((rc = rxg_tx_cksum_dev(c, &tb, st))) return rc;
+    if (arena_bytes) *arena_bytes = need;
+    return 0;
+}
+
+// ------------------------------------------------------------------ memory helpers ---
+extern "C" int rxg_dev_alloc(rxg_ctx *c, uint64_t bytes, void **out)
+{
+    if (!c || !out) return fail(-EINVAL, "rxg_dev_alloc: NULL argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIP_OK(hipMalloc(out, bytes ? bytes : 1));
+    return 0;
+}
+
+extern "C" int rxg_dev_free(rxg_ctx *c, void *p)
+{
+    if (!c) return fail(-EINVAL, "rxg_dev_free: ctx NULL");
+    if (p) HIP_OK(hipFree(p));
+    return 0;
+}
+
+extern "C" int rxg_host_alloc_pinned(rxg_ctx *c, uint64_t bytes, void **out)
+{
+    if (!c || !out) return fail(-EINVAL, "rxg_host_alloc_pinned: NULL argument");
+    HIP_OK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return 0;
+}
+
+extern "C" int rxg_host_free_pinned(rxg_ctx *c, void *p)
+{
+    if (!c) return fail(-EINVAL, "rxg_host_free_pinned: ctx NULL");
+    if (p) HIP_OK(hipHostFree(p));
+    return 0;
+}
+
+extern "C" int rxg_memcpy_h2d(rxg_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream)
+{
+    if (!c) return fail(-EINVAL, "rxg_memcpy_h2d: ctx NULL");
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_memcpy_d2h(rxg_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream)
+{
+    if (!c) return fail(-EINVAL, "rxg_memcpy_d2h: ctx NULL");
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_memset_dev(rxg_ctx *c, void *dst, int value, uint64_t bytes, void *stream)
+{
+    if (!c) return fail(-EINVAL, "rxg_memset_dev: ctx NULL");
+    HIP_OK(hipMemsetAsync(dst, value, bytes, pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_stream_sync(rxg_ctx *c, void *stream)
+{
+    if (!c) return fail(-EINVAL, "rxg_stream_sync: ctx NULL");
+    HIP_OK(hipStreamSynchronize(pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_event_create(rxg_ctx *c, rxg_event **out)
+{
+    if (!c || !out) return fail(-EINVAL, "rxg_event_create: NULL argument");
+    rxg_event *e = new rxg_event();
+    if (hipEventCreate(&e->e) != hipSuccess) {
+        delete e;
+        return fail(-EIO, "rxg_event_create: hipEventCreate failed");
+    }
+    *out = e;
+    return 0;
+}
+
+extern "C" int rxg_event_record(rxg_ctx *c, rxg_event *e, void *stream)
+{
+    if (!c || !e) return fail(-EINVAL, "rxg_event_record: NULL argument");
+    HIP_OK(hipEventRecord(e->e, pick(c, stream)));
+    return 0;
+}
+
+extern "C" int rxg_event_elapsed_ms(rxg_ctx *c, rxg_event *a, rxg_event *b, float *ms)
+{
+    if (!c || !a || !b || !ms) return fail(-EINVAL, "rxg_event_elapsed_ms: NULL argument");
+    HIP_OK(hipEventSynchronize(b->e));
+    HIP_OK(hipEventElapsedTime(ms, a->e, b->e));
+    return 0;
+}
+
+extern "C" int rxg_event_destroy(rxg_ctx *c, rxg_event *e)
+{
+    (void)c;
+    if (e) {
+        (void)hipEventDestroy(e->e);
+        delete e;
+    }
+    return 0;
+}

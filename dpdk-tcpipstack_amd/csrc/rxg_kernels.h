@@ -1,0 +1,34 @@
+// rxg_kernels.h — host-side launch interface of rxg_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "rxg_common.h"
+
+namespace rxg {
+
+struct LaunchRx {
+    const uint8_t *frames;
+    const uint32_t *off64;
+    const uint16_t *len;
+    uint32_t n;
+    int mode;              // 16 / 48: receive records of that size; 0: tx checksum generate
+    uint8_t *out;
+    DevTable table;
+    unsigned long long *counters;
+    uint32_t max_blocks;   // persistent grid cap (grid-stride over 64-frame slices)
+};
+
+struct LaunchSynth {
+    uint8_t *frames;
+    uint32_t *off64;
+    uint16_t *len;
+    uint32_t *flow;
+    uint64_t seed;
+    uint64_t arena_bytes;
+    uint32_t n, nflows, dst_ip, dport, mix, len_a;
+};
+
+hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
+hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);
+
+}  // namespace rxg

@@ -1,0 +1,572 @@
+// rxg_kernels.hip — gfx950 kernels of the rxg receive-path engine.
+//
+// One fused kernel replaces, for a whole batch, the reference's per-packet
+//   ether_in (etherin.c:12-37) -> ip_in (ip.c:19-42) -> tcp_in (tcp_in.c:32-84)
+//   -> findtcb (tcp_tcb.c:127-173)
+// plus the rx checksum the reference defines but compiles out (tcp_in.c:37, its
+// primitive calculate_checksum is ip.c:44-59).
+//
+// Work decomposition:
+//   * A wave owns a SLICE of 64 consecutive frames (one descriptor per lane: off64, len).
+//   * Frames are grouped by size class inside the wave (ballot + ds_permute compaction);
+//     each class is processed with LPF lanes per frame and NLOAD 16-byte loads per lane,
+//     so 64-byte frames run one frame per lane and 1500-byte frames 16 lanes per frame.
+//     No host binning, no second launch, any size mix.
+//   * Checksums: one's-complement sums are byte-order independent (RFC 1071 §2(B)), so
+//     lanes add little-endian 16-bit halves of the loaded dwords and the final fold is
+//     byte-swapped once: bit-exact with the reference's big-endian byte loop.
+//   * Classify: exact-tuple hash (4 slots per 64-byte bucket, value = lowest tcbs[] index
+//     with that tuple) then the dport listener map: pass 1 / pass 2 of findtcb.
+//   * Counters: wave-uniform ballot counts, one u64 atomic per counter per workgroup.
+#include <hip/hip_runtime.h>
+
+#include "rxg_common.h"
+#include "rxg_kernels.h"
+
+namespace rxg {
+
+// --------------------------------------------------------------------------- helpers ---
+
+__device__ __forceinline__ uint32_t hsum(uint32_t d) { return (d & 0xFFFFu) + (d >> 16); }
+
+// Bytes [lo, hi) of the little-endian dword at frame offset o (o % 4 == 0).
+__device__ __forceinline__ uint32_t region_mask(int o, int lo, int hi)
+{
+    int a = min(max(lo - o, 0), 4);
+    int b = min(max(hi - o, 0), 4);
+    uint32_t mb = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    uint32_t ma = a >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a)) - 1u);
+    return b > a ? (mb & ~ma) : 0u;
+}
+
+// Keep the low `keep` bytes (0..4) of a dword.
+__device__ __forceinline__ uint32_t keep_low(uint32_t d, int keep)
+{
+    return keep >= 4 ? d : (keep <= 0 ? 0u : (d & ((1u << (8 * keep)) - 1u)));
+}
+
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, int src_lane)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+__device__ __forceinline__ uint4 load16(const uint8_t *p)
+{
+#if RXG_NT_LOADS
+    return __builtin_nontemporal_load(reinterpret_cast<const uint4 *>(p));
+#else
+    return *reinterpret_cast<const uint4 *>(p);
+#endif
+}
+
+// Dword K (bytes 4K..4K+3, K < 12) of the frame owned by the lane group starting at gbase.
+// Chunk c = K/4 is held by lane gbase + c % LPF in its register j = c / LPF.
+template <int K, int LPF, int NLOAD>
+__device__ __forceinline__ uint32_t hdr_dword(const uint32_t (&d)[NLOAD][4], int gbase)
+{
+    constexpr int c = K / 4, w = K % 4, j = c / LPF, src = c % LPF;
+    static_assert(j < NLOAD, "header chunk must be in the first load set");
+    if constexpr (LPF == 1)
+        return d[j][w];
+    else
+        return lane_read(d[j][w], gbase + src);
+}
+
+struct WaveCounters {
+    uint32_t c[RXG_NCOUNTERS];
+};
+
+__device__ __forceinline__ void wcount(WaveCounters &wc, int k, bool pred)
+{
+    wc.c[k] += (uint32_t)__popcll(__ballot(pred));
+}
+
+struct RxArgs {
+    const uint8_t *frames;
+    const uint32_t *off64;
+    const uint16_t *len;
+    uint32_t n;
+    uint32_t pad;
+    uint8_t *out;
+    DevTable t;
+    unsigned long long *counters;
+};
+
+// ------------------------------------------------------------- one round of frames ---
+//
+// MODE 16 / 48: receive (records of that size).  MODE 0: transmit checksum generate.
+template <int LPF, int NLOAD, bool JUMBO, int MODE>
+__device__ __forceinline__ void frame_round(const RxArgs &a, uint32_t f, uint32_t off, uint32_t len,
+                                            bool active, int lane, WaveCounters &wc)
+{
+    constexpr bool TX = MODE == 0;
+    const int gl = lane & (LPF - 1);
+    const int gbase = lane - gl;
+    const bool leader = active && gl == 0;
+    uint8_t *fp = const_cast<uint8_t *>(a.frames) + (size_t)off * 64u;
+
+    uint32_t d[NLOAD][4];
+#pragma unroll
+    for (int j = 0; j < NLOAD; ++j) {
+        const int c = gl + j * LPF;
+        if (active && (uint32_t)(c * 16) < len) {
+            uint4 v = load16(fp + c * 16);
+            d[j][0] = v.x; d[j][1] = v.y; d[j][2] = v.z; d[j][3] = v.w;
+        } else {
+            d[j][0] = d[j][1] = d[j][2] = d[j][3] = 0u;
+        }
+    }
+
+    // ---- header: dwords 1..11 (bytes 4..47) of the group's frame, gathered to every lane.
+    uint32_t h1 = 0, h2 = 0;
+    if constexpr (MODE == 48) {
+        h1 = hdr_dword<1, LPF, NLOAD>(d, gbase);
+        h2 = hdr_dword<2, LPF, NLOAD>(d, gbase);
+    }
+    uint32_t h3 = hdr_dword<3, LPF, NLOAD>(d, gbase);
+    uint32_t h4 = hdr_dword<4, LPF, NLOAD>(d, gbase);
+    uint32_t h5 = hdr_dword<5, LPF, NLOAD>(d, gbase);
+    uint32_t h6 = hdr_dword<6, LPF, NLOAD>(d, gbase);
+    uint32_t h7 = hdr_dword<7, LPF, NLOAD>(d, gbase);
+    uint32_t h8 = hdr_dword<8, LPF, NLOAD>(d, gbase);
+    uint32_t h9 = hdr_dword<9, LPF, NLOAD>(d, gbase);
+    uint32_t h10 = hdr_dword<10, LPF, NLOAD>(d, gbase);
+    uint32_t h11 = hdr_dword<11, LPF, NLOAD>(d, gbase);
+
+    const bool trunc = len < 54u;
+    if (trunc) {  // bytes at/after data_len read as zero (reference: stale mbuf bytes)
+        const int L = (int)len;
+        h1 = keep_low(h1, L - 4);   h2 = keep_low(h2, L - 8);   h3 = keep_low(h3, L - 12);
+        h4 = keep_low(h4, L - 16);  h5 = keep_low(h5, L - 20);  h6 = keep_low(h6, L - 24);
+        h7 = keep_low(h7, L - 28);  h8 = keep_low(h8, L - 32);  h9 = keep_low(h9, L - 36);
+        h10 = keep_low(h10, L - 40); h11 = keep_low(h11, L - 44);
+    }
+
+    const uint32_t et = bswap16(h3 & 0xFFFFu);          // etherin.c:21
+    const uint32_t vihl = (h3 >> 16) & 0xFFu;
+    const uint32_t tl = bswap16(h4 & 0xFFFFu);          // ip total_length
+    const uint32_t proto = h5 >> 24;                    // ip.c:28
+    const uint32_t src_raw = (h6 >> 16) | (h7 << 16);   // bytes 26..29
+    const uint32_t dst_raw = (h7 >> 16) | (h8 << 16);   // bytes 30..33
+    const uint32_t sport = bswap16(h8 >> 16);           // tcp_tcb.c:135
+    const uint32_t dport = bswap16(h9 & 0xFFFFu);       // tcp_tcb.c:134
+    const uint32_t seq_raw = (h9 >> 16) | (h10 << 16);
+    const uint32_t ack_raw = (h10 >> 16) | (h11 << 16);
+    const uint32_t doff = (h11 >> 16) & 0xFFu;
+    const uint32_t tflags = h11 >> 24;
+
+    // TCP span = pseudo(src,dst from bytes 26..33) || segment [34, E), E = 14 + total_length,
+    // clamped to data_len; bytes [26, 48) come from the gathered header, [48, end) from
+    // the lanes' chunks c >= 3.
+    const int E = max(34, 14 + (int)tl);
+    const int tcp_end = min((int)len, E);
+
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int j = 0; j < NLOAD; ++j) {
+        const int c = gl + j * LPF;
+        const int o = c * 16;
+        if (c >= 3) {
+            if constexpr (TX) {  // the cksum field (bytes 50-51) is zero while summing
+                if (c == 3) d[j][0] &= 0x0000FFFFu;
+            }
+            if (o + 16 <= tcp_end) {
+                tsum += hsum(d[j][0]) + hsum(d[j][1]) + hsum(d[j][2]) + hsum(d[j][3]);
+            } else {
+                tsum += hsum(keep_low(d[j][0], tcp_end - o)) + hsum(keep_low(d[j][1], tcp_end - o - 4)) +
+                        hsum(keep_low(d[j][2], tcp_end - o - 8)) + hsum(keep_low(d[j][3], tcp_end - o - 12));
+            }
+        }
+    }
+    if constexpr (JUMBO) {
+        // frames beyond LPF*NLOAD chunks: keep streaming LPF chunks per step
+        for (int base = LPF * NLOAD; base * 16 < (int)len; base += LPF) {
+            const int c = base + gl;
+            const int o = c * 16;
+            if (active && o < tcp_end) {
+                uint4 v = load16(fp + o);
+                if (o + 16 <= tcp_end)
+                    tsum += hsum(v.x) + hsum(v.y) + hsum(v.z) + hsum(v.w);
+                else
+                    tsum += hsum(keep_low(v.x, tcp_end - o)) + hsum(keep_low(v.y, tcp_end - o - 4)) +
+                            hsum(keep_low(v.z, tcp_end - o - 8)) + hsum(keep_low(v.w, tcp_end - o - 12));
+            }
+        }
+    }
+#pragma unroll
+    for (int m = LPF / 2; m > 0; m >>= 1)
+        tsum += (uint32_t)__shfl_xor((int)tsum, m, 64);
+
+    // Header parts of both sums (bytes beyond data_len are already zero in h*).
+    uint32_t h6_ip = TX ? (h6 & 0xFFFF0000u) : h6;   // TX: hdr_checksum (bytes 24-25) = 0
+    const uint32_t isum = hsum(h3 & 0xFFFF0000u) + hsum(h4) + hsum(h5) + hsum(h6_ip) + hsum(h7) +
+                          hsum(h8 & 0xFFFFu);
+    const uint32_t thdr = hsum(h6 & 0xFFFF0000u) + hsum(h7) + hsum(h8 & region_mask(32, 26, E)) +
+                          hsum(h9 & region_mask(36, 26, E)) + hsum(h10 & region_mask(40, 26, E)) +
+                          hsum(h11 & region_mask(44, 26, E));
+    // pseudo {.., 0x00, 0x06, htons(total_length - 20)} as little-endian words
+    const uint32_t tall = tsum + thdr + 0x0600u + bswap16((tl - 20u) & 0xFFFFu);
+    const uint32_t ip_ck = (~bswap16(fold16(isum))) & 0xFFFFu;
+    const uint32_t tcp_ck = (~bswap16(fold16(tall))) & 0xFFFFu;
+
+    if constexpr (TX) {
+        // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118)
+        if (leader) {
+            if (len > 25u) *reinterpret_cast<uint16_t *>(fp + 24) = (uint16_t)bswap16(ip_ck);
+            if (len > 51u) *reinterpret_cast<uint16_t *>(fp + 50) = (uint16_t)bswap16(tcp_ck);
+            else if (len > 50u) fp[50] = (uint8_t)(tcp_ck >> 8);
+        }
+        wcount(wc, RXG_C_RX, leader);
+        return;
+    } else {
+        const bool is_ip = et == RXG_ETHER_TYPE_IPV4;
+        const bool is_tcp = is_ip && proto == RXG_IPPROTO_TCP;
+        const uint32_t src_host = bswap32(src_raw);
+
+        // ---- findtcb (tcp_tcb.c:127-173)
+        int32_t idx = -1;
+        bool lhit = false, nslot = false;
+        uint32_t st = RXG_STATE_NONE;
+        if (leader && is_tcp) {
+            const uint32_t ports = (dport << 16) | sport;
+            uint32_t hb = tuple_hash(ports, dst_raw, src_host) & a.t.bucket_mask;
+            for (uint32_t probe = 0; probe <= a.t.bucket_mask; ++probe) {
+                const uint4 *b = a.t.buckets + (size_t)hb * kSlotsPerBucket;
+                const uint4 s0 = b[0], s1 = b[1], s2 = b[2], s3 = b[3];
+                if (s0.x == ports && s0.y == dst_raw && s0.z == src_host && s0.w != kEmpty) idx = (int32_t)s0.w;
+                if (s1.x == ports && s1.y == dst_raw && s1.z == src_host && s1.w != kEmpty) idx = (int32_t)s1.w;
+                if (s2.x == ports && s2.y == dst_raw && s2.z == src_host && s2.w != kEmpty) idx = (int32_t)s2.w;
+                if (s3.x == ports && s3.y == dst_raw && s3.z == src_host && s3.w != kEmpty) idx = (int32_t)s3.w;
+                const bool any_empty = s0.w == kEmpty || s1.w == kEmpty || s2.w == kEmpty || s3.w == kEmpty;
+                if (idx >= 0 || any_empty) break;
+                hb = (hb + 1u) & a.t.bucket_mask;
+            }
+            if (idx < 0) {  // pass 2: first LISTENING slot on dport
+                const int32_t L = a.t.listen[dport];
+                idx = L;
+                lhit = L >= 0;
+                nslot = a.t.min_null < (L >= 0 ? L : a.t.ntcb);
+            }
+            if (idx >= 0) st = a.t.state[idx];
+        }
+
+        // ---- verdict (etherin.c:21-35, ip.c:28-39, tcp_in.c:47-72)
+        uint32_t verdict;
+        if (!is_ip)
+            verdict = et == RXG_ETHER_TYPE_ARP ? RXG_V_ARP : RXG_V_DROP_L2;
+        else if (!is_tcp)
+            verdict = RXG_V_DROP_NONTCP;
+        else if (idx < 0)
+            verdict = RXG_V_RST_NOPCB;
+        else if (st == RXG_LISTENING && !(tflags & RXG_TCP_FLAG_SYN))
+            verdict = RXG_V_RST_LISTEN_NONSYN;
+        else
+            verdict = RXG_V_DISPATCH;
+
+        const uint32_t ipc = is_ip ? ip_ck : 0u;
+        const uint32_t tcc = is_tcp ? tcp_ck : 0u;
+        const uint32_t flags = ((is_ip && ipc == 0u) ? RXG_F_IP_OK : 0u) |
+                               ((is_tcp && tcc == 0u) ? RXG_F_TCP_OK : 0u) |
+                               (lhit ? RXG_F_LISTEN : 0u) | (nslot ? RXG_F_REF_NULLSLOT : 0u) |
+                               (trunc ? RXG_F_TRUNC : 0u);
+        const int32_t datalen = (int32_t)tl - (int32_t)(vihl & 0xFu) * 4 - (int32_t)(doff >> 4) * 4;
+
+        if (leader) {
+            uint4 q0;
+            q0.x = (uint32_t)idx;
+            q0.y = ipc | (tcc << 16);
+            q0.z = verdict | (st << 8) | (tflags << 16) | (flags << 24);
+            q0.w = (uint32_t)datalen;
+            uint4 *rec = reinterpret_cast<uint4 *>(a.out + (size_t)f * MODE);
+            rec[0] = q0;
+            if constexpr (MODE == 48) {
+                uint4 q1, q2;
+                q1.x = et | (sport << 16);
+                q1.y = dport | (proto << 16) | (vihl << 24);
+                q1.z = bswap32(seq_raw);
+                q1.w = bswap32(ack_raw);
+                q2.x = src_host;
+                q2.y = dst_raw;
+                q2.z = doff | ((h1 >> 16) << 8) | ((h2 & 0xFFu) << 24);
+                q2.w = h2 >> 8;
+                rec[1] = q1;
+                rec[2] = q2;
+            }
+        }
+
+        // ---- counters (definition: oracle orc_count_record)
+        const bool is_arp = et == RXG_ETHER_TYPE_ARP;
+        wcount(wc, RXG_C_RX, leader);
+        wcount(wc, RXG_C_TRUNC, leader && trunc);
+        wcount(wc, RXG_C_IPV4, leader && is_ip);
+        wcount(wc, RXG_C_ARP, leader && is_arp);
+        wcount(wc, RXG_C_OTHER_L2, leader && !is_ip && !is_arp);
+        wcount(wc, RXG_C_IP_CKSUM_BAD, leader && is_ip && ipc != 0u);
+        wcount(wc, RXG_C_TCP, leader && is_tcp);
+        wcount(wc, RXG_C_NON_TCP, leader && is_ip && !is_tcp);
+        wcount(wc, RXG_C_TCP_CKSUM_BAD, leader && is_tcp && tcc != 0u);
+        wcount(wc, RXG_C_REF_NULLSLOT, leader && is_tcp && nslot);
+        wcount(wc, RXG_C_TCB_HIT_EXACT, leader && is_tcp && idx >= 0 && !lhit);
+        wcount(wc, RXG_C_TCB_HIT_LISTEN, leader && is_tcp && lhit);
+        wcount(wc, RXG_C_NOPCB, leader && verdict == RXG_V_RST_NOPCB);
+        wcount(wc, RXG_C_LISTEN_NONSYN, leader && verdict == RXG_V_RST_LISTEN_NONSYN);
+        wcount(wc, RXG_C_DISPATCH, leader && verdict == RXG_V_DISPATCH);
+    }
+}
+
+// ---------------------------------------------------------- size-class dispatch ---
+//
+// Class c of a frame, by data_len:  <=64 | <=128 | <=256 | <=512 | <=1024 | <=1536 | <=2048 | more
+__device__ __forceinline__ int size_class(uint32_t len)
+{
+    return len <= 64u ? 0 : len <= 128u ? 1 : len <= 256u ? 2 : len <= 512u ? 3
+         : len <= 1024u ? 4 : len <= 1536u ? 5 : len <= 2048u ? 6 : 7;
+}
+
+template <int C, int LPF, int NLOAD, bool JUMBO, int MODE>
+__device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t f, uint32_t off,
+                                          uint32_t len, int lane, WaveCounters &wc)
+{
+    constexpr int FPW = 64 / LPF;
+    const unsigned long long m = __ballot(cls == C);
+    if (m == 0ull) return;
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    uint32_t cf = f, coff = off, clen = len;
+    if (m != ~0ull) {
+        // compact this class's frames to lanes 0..cnt-1, keeping their order
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t dst = (cls == C) ? below : cnt + ((uint32_t)lane - below);
+        cf = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)f);
+        coff = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)off);
+        clen = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)len);
+    }
+    for (uint32_t r = 0; r < cnt; r += FPW) {
+        const uint32_t k = r + (uint32_t)(lane / LPF);
+        const bool act = k < cnt;
+        uint32_t kf, koff, klen;
+        if constexpr (LPF == 1) {
+            kf = cf; koff = coff; klen = clen;
+        } else {
+            const int src = (int)(k & 63u);
+            kf = lane_read(cf, src);
+            koff = lane_read(coff, src);
+            klen = lane_read(clen, src);
+        }
+        frame_round<LPF, NLOAD, JUMBO, MODE>(a, kf, koff, act ? klen : 0u, act, lane, wc);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
+{
+    __shared__ unsigned long long s_cnt[4][RXG_NCOUNTERS];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
+    const uint32_t nwaves = gridDim.x * 4u;
+    const uint32_t nslices = (a.n + 63u) >> 6;
+
+    WaveCounters wc;
+#pragma unroll
+    for (int k = 0; k < RXG_NCOUNTERS; ++k) wc.c[k] = 0u;
+    unsigned long long bytes = 0ull;
+
+    for (uint32_t s = wave; s < nslices; s += nwaves) {
+        const uint32_t f = s * 64u + (uint32_t)lane;
+        const bool valid = f < a.n;
+        const uint32_t off = valid ? a.off64[f] : 0u;
+        const uint32_t len = valid ? (uint32_t)a.len[f] : 0u;
+        const int cls = valid ? size_class(len) : 8;
+        bytes += len;
+        run_class<0, 1, 4, false, MODE>(a, cls, f, off, len, lane, wc);
+        run_class<1, 2, 4, false, MODE>(a, cls, f, off, len, lane, wc);
+        run_class<2, 4, 4, false, MODE>(a, cls, f, off, len, lane, wc);
+        run_class<3, 8, 4, false, MODE>(a, cls, f, off, len, lane, wc);
+        run_class<4, 16, 4, false, MODE>(a, cls, f, off, len, lane, wc);
+        run_class<5, 16, 6, false, MODE>(a, cls, f, off, len, lane, wc);
+        run_class<6, 32, 4, false, MODE>(a, cls, f, off, len, lane, wc);
+        run_class<7, 64, 2, true, MODE>(a, cls, f, off, len, lane, wc);
+    }
+
+    if (a.counters == nullptr) return;
+    // wave -> workgroup -> one atomic per counter
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        const unsigned long long o = __shfl_xor(bytes, m, 64);
+        bytes += o;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < RXG_NCOUNTERS; ++k) s_cnt[wid][k] = wc.c[k];
+        if (MODE != 0) s_cnt[wid][RXG_C_BYTES] = bytes;
+    }
+    __syncthreads();
+    if (threadIdx.x < RXG_NCOUNTERS) {
+        const int k = threadIdx.x;
+        const unsigned long long v = s_cnt[0][k] + s_cnt[1][k] + s_cnt[2][k] + s_cnt[3][k];
+        if (v) atomicAdd(&a.counters[k], v);
+    }
+}
+
+// ------------------------------------------------------------------ synthetic frames ---
+struct SynthArgs {
+    uint8_t *frames;
+    uint32_t *off64;
+    uint16_t *len;
+    uint32_t *flow;
+    uint64_t seed;
+    uint64_t nchunks;   // 16-byte chunks of the arena
+    uint32_t n;
+    uint32_t nflows;
+    uint32_t dst_ip;    // host order
+    uint32_t dport;
+    uint32_t mix;
+    uint32_t len_a;
+    uint32_t slots_a;   // 64-byte slots per frame (mix 0)
+};
+
+__device__ __forceinline__ uint8_t synth_hdr_byte(int i, uint32_t frame, uint32_t flow, uint32_t L,
+                                                  const SynthArgs &s, uint32_t seq, uint32_t ack)
+{
+    const uint32_t tl = L - 14u;
+    const uint32_t sport = 1024u + flow % 64511u;
+    switch (i) {
+    case 0: return 0x02; case 1: return 0x00; case 2: return 0xC0; case 3: return 0xA8;
+    case 4: return 0x4E; case 5: return 0x02;                         // dst MAC
+    case 6: return 0x02; case 7: return 0x00; case 8: return 0x0A;
+    case 9: return (uint8_t)(flow >> 16); case 10: return (uint8_t)(flow >> 8);
+    case 11: return (uint8_t)flow;                                    // src MAC
+    case 12: return 0x08; case 13: return 0x00;                       // IPv4
+    case 14: return 0x45; case 15: return 0x00;
+    case 16: return (uint8_t)(tl >> 8); case 17: return (uint8_t)tl;
+    case 18: return (uint8_t)(frame >> 8); case 19: return (uint8_t)frame;
+    case 20: return 0x40; case 21: return 0x00;                       // DF
+    case 22: return 64; case 23: return RXG_IPPROTO_TCP;
+    case 24: case 25: return 0;                                       // filled by tx kernel
+    case 26: return 10; case 27: return (uint8_t)(flow >> 16);
+    case 28: return (uint8_t)(flow >> 8); case 29: return (uint8_t)flow;
+    case 30: return (uint8_t)(s.dst_ip >> 24); case 31: return (uint8_t)(s.dst_ip >> 16);
+    case 32: return (uint8_t)(s.dst_ip >> 8); case 33: return (uint8_t)s.dst_ip;
+    case 34: return (uint8_t)(sport >> 8); case 35: return (uint8_t)sport;
+    case 36: return (uint8_t)(s.dport >> 8); case 37: return (uint8_t)s.dport;
+    case 38: return (uint8_t)(seq >> 24); case 39: return (uint8_t)(seq >> 16);
+    case 40: return (uint8_t)(seq >> 8); case 41: return (uint8_t)seq;
+    case 42: return (uint8_t)(ack >> 24); case 43: return (uint8_t)(ack >> 16);
+    case 44: return (uint8_t)(ack >> 8); case 45: return (uint8_t)ack;
+    case 46: return 0x50; case 47: return RXG_TCP_FLAG_ACK;
+    case 48: return 0xFF; case 49: return 0xFF;                       // window
+    default: return 0;                                                // cksum, urg
+    }
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(SynthArgs s)
+{
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < s.nchunks; t += (uint64_t)gridDim.x * 256ull) {
+        uint32_t frame, c, L;
+        uint64_t frame_slot;
+        if (s.mix == 0) {
+            const uint64_t cps = (uint64_t)s.slots_a * 4u;
+            frame = (uint32_t)(t / cps);
+            c = (uint32_t)(t % cps);
+            L = s.len_a;
+            frame_slot = (uint64_t)frame * s.slots_a;
+        } else {
+            const uint64_t cpb = (uint64_t)kImixSlotsPerBlock * 4u;
+            const uint64_t blk = t / cpb;
+            uint32_t rem = (uint32_t)(t % cpb);
+            const uint32_t rot = (uint32_t)(splitmix64(s.seed ^ 0xB10Cull ^ blk) % kImixBlock);
+            uint32_t slot = 0, pos = 0;
+            for (;;) {
+                const uint32_t l = imix_len((int)((pos + rot) % kImixBlock));
+                const uint32_t chunks = ((l + 63u) / 64u) * 4u;
+                if (rem < chunks) { L = l; break; }
+                rem -= chunks;
+                slot += chunks / 4u;
+                ++pos;
+            }
+            frame = (uint32_t)(blk * kImixBlock + pos);
+            c = rem;
+            frame_slot = blk * kImixSlotsPerBlock + slot;
+        }
+        if (frame >= s.n) continue;
+        const uint64_t fr = splitmix64(0x5EED0002ull ^ s.seed ^ ((uint64_t)frame << 1));
+        const uint32_t flow = (uint32_t)(fr % s.nflows);
+        const uint64_t sa = splitmix64(s.seed ^ 0xA5A5ull ^ ((uint64_t)frame << 2));
+        const uint32_t seq = (uint32_t)sa, ack = (uint32_t)(sa >> 32);
+        if (c == 0) {
+            s.off64[frame] = (uint32_t)frame_slot;
+            s.len[frame] = (uint16_t)L;
+            if (s.flow) s.flow[frame] = flow;
+        }
+        uint8_t b[16];
+        const uint64_t p0 = splitmix64(0x5EED0001ull ^ s.seed ^ ((uint64_t)frame << 12) ^ (2u * c));
+        const uint64_t p1 = splitmix64(0x5EED0001ull ^ s.seed ^ ((uint64_t)frame << 12) ^ (2u * c + 1u));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t bi = c * 16u + (uint32_t)i;
+            uint8_t v;
+            if (bi >= L) v = 0;
+            else if (bi < 54u) v = synth_hdr_byte((int)bi, frame, flow, L, s, seq, ack);
+            else v = (uint8_t)((i < 8 ? p0 : p1) >> (8 * (i & 7)));
+            b[i] = v;
+        }
+        uint4 q;
+        q.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+        q.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+        q.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
+        q.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
+        *reinterpret_cast<uint4 *>(s.frames + (frame_slot * 64u) + c * 16u) = q;
+    }
+}
+
+// ------------------------------------------------------------------ launch wrappers ---
+
+hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
+{
+    RxArgs a;
+    a.frames = L.frames;
+    a.off64 = L.off64;
+    a.len = L.len;
+    a.n = L.n;
+    a.pad = 0;
+    a.out = L.out;
+    a.t = L.table;
+    a.counters = L.counters;
+    if (L.n == 0) return hipSuccess;
+    const uint32_t nslices = (L.n + 63u) / 64u;
+    uint32_t blocks = (nslices + 3u) / 4u;
+    if (blocks > L.max_blocks) blocks = L.max_blocks;
+    if (L.mode == 16)
+        hipLaunchKernelGGL(rx_kernel<16>, dim3(blocks), dim3(256), 0, st, a);
+    else if (L.mode == 48)
+        hipLaunchKernelGGL(rx_kernel<48>, dim3(blocks), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(rx_kernel<0>, dim3(blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(const LaunchSynth &L, hipStream_t st)
+{
+    SynthArgs s;
+    s.frames = L.frames;
+    s.off64 = L.off64;
+    s.len = L.len;
+    s.flow = L.flow;
+    s.seed = L.seed;
+    s.nchunks = L.arena_bytes / 16u;
+    s.n = L.n;
+    s.nflows = L.nflows ? L.nflows : 1u;
+    s.dst_ip = L.dst_ip;
+    s.dport = L.dport;
+    s.mix = L.mix;
+    s.len_a = L.len_a;
+    s.slots_a = (L.len_a + 63u) / 64u;
+    if (s.nchunks == 0) return hipSuccess;
+    uint64_t blocks = (s.nchunks + 255u) / 256u;
+    if (blocks > 16384u) blocks = 16384u;
+    hipLaunchKernelGGL(synth_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, s);
+    return hipGetLastError();
+}
+
+}  // namespace rxg

@@ -1,0 +1,436 @@
+"""rxg — Python binding of the MI355X receive-path engine's C ABI (include/rxg.h).
+
+This is a thin ctypes layer used by tests/, bench.py and __graft_entry__.py; the engine
+itself is librxg.so (HIP kernels for gfx950 + C++ host code).  There is no Python or CPU
+compute path: if librxg.so is missing, or no GPU is present, calls raise RxgError.
+
+The reference surface this mirrors (rajneshrat/dpdk-tcpipstack, tcp_ip_stack/):
+  ether_in/ip_in/tcp_in/findtcb per packet    -> Engine.rx_burst_dev / Engine.rx_burst
+  tcbs[] writes (alloc_tcb, remove_tcb, state) -> Engine.tcb_upsert / tcb_remove / tcb_set_state
+  ip_out's two checksums (ip.c:97-118)        -> Engine.tx_cksum_dev
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librxg.so")
+
+# ---------------------------------------------------------------- constants (rxg.h) ---
+ETHER_TYPE_IPV4 = 0x0800
+ETHER_TYPE_ARP = 0x0806
+IPPROTO_TCP = 6
+TCP_FLAG_FIN, TCP_FLAG_SYN, TCP_FLAG_RST, TCP_FLAG_PSH, TCP_FLAG_ACK = 1, 2, 4, 8, 16
+(TCP_STATE_CLOSED, LISTENING, SYN_SENT, SYN_RECV, TCP_ESTABLISHED, TCP_STATE_FIN_1,
+ TCP_FIN_2) = range(7)
+STATE_NONE = 0xFF
+
+V_DISPATCH, V_RST_NOPCB, V_RST_LISTEN_NONSYN, V_DROP_NONTCP, V_ARP, V_DROP_L2 = range(6)
+F_IP_OK, F_TCP_OK, F_LISTEN, F_REF_NULLSLOT, F_TRUNC, F_ARP_LEARN = 1, 2, 4, 8, 16, 32
+REC16, REC48 = 16, 48
+
+COUNTERS = ["rx", "bytes", "ipv4", "arp", "other_l2", "tcp", "non_tcp", "ip_cksum_bad",
+            "tcp_cksum_bad", "tcb_hit_exact", "tcb_hit_listen", "nopcb", "listen_nonsyn",
+            "dispatch", "ref_nullslot", "trunc"]
+NCOUNTERS = len(COUNTERS)
+
+# numpy views of the C records
+REC16_DTYPE = np.dtype([("tcb_idx", "<i4"), ("ip_cksum", "<u2"), ("tcp_cksum", "<u2"),
+                        ("verdict", "u1"), ("state", "u1"), ("tcp_flags", "u1"),
+                        ("flags", "u1"), ("datalen", "<i4")])
+REC48_DTYPE = np.dtype([("c", REC16_DTYPE), ("ether_type", "<u2"), ("sport", "<u2"),
+                        ("dport", "<u2"), ("l4_proto", "u1"), ("version_ihl", "u1"),
+                        ("seq", "<u4"), ("ack", "<u4"), ("src_ip", "<u4"),
+                        ("dst_ip_raw", "<u4"), ("data_off", "u1"), ("src_mac", "u1", (6,)),
+                        ("reserved", "u1")])
+TCB_DTYPE = np.dtype([("dport", "<i4"), ("sport", "<i4"), ("ipv4_dst", "<u4"),
+                      ("ipv4_src", "<u4"), ("state", "u1"), ("pad", "u1"),
+                      ("identifier", "<u2")])
+assert REC16_DTYPE.itemsize == 16 and REC48_DTYPE.itemsize == 48 and TCB_DTYPE.itemsize == 20
+
+
+class RxgError(RuntimeError):
+    pass
+
+
+# ------------------------------------------------------------------- ctypes structs ---
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("max_batch", C.c_uint32), ("max_bytes", C.c_uint32),
+                ("flags", C.c_uint32)]
+
+
+class TcbTuple(C.Structure):
+    _fields_ = [("dport", C.c_int32), ("sport", C.c_int32), ("ipv4_dst", C.c_uint32),
+                ("ipv4_src", C.c_uint32), ("state", C.c_uint8), ("pad", C.c_uint8),
+                ("identifier", C.c_uint16)]
+
+
+class DevBatch(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("off64", C.c_void_p), ("len", C.c_void_p),
+                ("n", C.c_uint32), ("rec_kind", C.c_uint32), ("out", C.c_void_p)]
+
+
+class DevTxBatch(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("off64", C.c_void_p), ("len", C.c_void_p),
+                ("n", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class PktView(C.Structure):
+    _fields_ = [("buf_addr", C.c_void_p), ("data_off", C.c_uint16), ("data_len", C.c_uint16),
+                ("pad", C.c_uint32)]
+
+
+class SynthParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n", C.c_uint32), ("nflows", C.c_uint32),
+                ("dst_ip_host", C.c_uint32), ("dport", C.c_uint16), ("mix", C.c_uint16),
+                ("len_a", C.c_uint16), ("pad", C.c_uint16)]
+
+
+HANDOFF_FREE = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p)
+HANDOFF_ARP_IN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p)
+HANDOFF_GET_MAC = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_void_p)
+HANDOFF_ADD_MAC = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_void_p)
+HANDOFF_SEND_RESET = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_void_p)
+HANDOFF_ON_SEGMENT = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_uint32, C.c_uint32)
+HANDOFF_TCPSWITCH = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.c_uint8, C.c_void_p,
+                                C.c_void_p, C.c_void_p)
+
+
+class HandoffOps(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("free_mbuf", HANDOFF_FREE), ("arp_in", HANDOFF_ARP_IN),
+                ("get_mac", HANDOFF_GET_MAC), ("add_mac", HANDOFF_ADD_MAC),
+                ("send_reset", HANDOFF_SEND_RESET), ("on_segment", HANDOFF_ON_SEGMENT),
+                ("tcpswitch", HANDOFF_TCPSWITCH)]
+
+
+# ------------------------------------------------------------------------- loading ---
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load librxg.so.  torch (if installed) is imported first so that librxg binds to the
+    same HIP runtime copy torch loaded (one HIP runtime per process)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RxgError(f"librxg.so not built: {path} (run __graft_entry__.build())")
+    if "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is optional for the binding
+            pass
+    lib = C.CDLL(path)
+    vp, u32, i32, u64 = C.c_void_p, C.c_uint32, C.c_int32, C.c_uint64
+    sig = {
+        "rxg_abi_version": (C.c_int, []),
+        "rxg_build_info": (C.c_char_p, []),
+        "rxg_last_error": (C.c_char_p, []),
+        "rxg_init": (C.c_int, [C.POINTER(Config), C.POINTER(vp)]),
+        "rxg_fini": (C.c_int, [vp]),
+        "rxg_sync": (C.c_int, [vp]),
+        "rxg_stream": (vp, [vp]),
+        "rxg_tcb_upsert": (C.c_int, [vp, i32, C.POINTER(TcbTuple)]),
+        "rxg_tcb_remove": (C.c_int, [vp, i32]),
+        "rxg_tcb_set_state": (C.c_int, [vp, i32, C.c_uint8]),
+        "rxg_tcb_load": (C.c_int, [vp, vp, vp, i32]),
+        "rxg_tcb_sync": (C.c_int, [vp]),
+        "rxg_tcb_count": (i32, [vp]),
+        "rxg_rx_burst_dev": (C.c_int, [vp, C.POINTER(DevBatch), vp]),
+        "rxg_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
+        "rxg_tx_cksum_dev": (C.c_int, [vp, C.POINTER(DevTxBatch), vp]),
+        "rxg_counters_reset": (C.c_int, [vp, vp]),
+        "rxg_counters_read": (C.c_int, [vp, vp]),
+        "rxg_counters_dev": (vp, [vp]),
+        "rxg_rx_replay": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, vp, u32, u32]),
+        "rxg_synth_dev": (C.c_int, [vp, C.POINTER(SynthParams), vp, u64, vp, vp, vp,
+                                    C.POINTER(u64), vp]),
+        "rxg_synth_arena_bytes": (u64, [C.POINTER(SynthParams)]),
+        "rxg_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
+        "rxg_dev_free": (C.c_int, [vp, vp]),
+        "rxg_host_alloc_pinned": (C.c_int, [vp, u64, C.POINTER(vp)]),
+        "rxg_host_free_pinned": (C.c_int, [vp, vp]),
+        "rxg_memcpy_h2d": (C.c_int, [vp, vp, vp, u64, vp]),
+        "rxg_memcpy_d2h": (C.c_int, [vp, vp, vp, u64, vp]),
+        "rxg_memset_dev": (C.c_int, [vp, vp, C.c_int, u64, vp]),
+        "rxg_stream_sync": (C.c_int, [vp, vp]),
+        "rxg_event_create": (C.c_int, [vp, C.POINTER(vp)]),
+        "rxg_event_record": (C.c_int, [vp, vp, vp]),
+        "rxg_event_elapsed_ms": (C.c_int, [vp, vp, vp, C.POINTER(C.c_float)]),
+        "rxg_event_destroy": (C.c_int, [vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.rxg_abi_version() != 1:
+        raise RxgError("librxg ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.rxg_last_error().decode(errors="replace") if _lib else ""
+        raise RxgError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# ------------------------------------------------------------------------- helpers ---
+def pack_arena(frames: list[bytes]) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Pack frames at 64-byte aligned starts (the rxg batch layout).
+    Returns (arena u8, off64 u32, len u16)."""
+    n = len(frames)
+    lens = np.fromiter((len(f) for f in frames), dtype=np.uint32, count=n)
+    if n and lens.max() > 0xFFFF:
+        raise ValueError("frame longer than 65535 bytes")
+    slots = (lens + 63) // 64
+    off = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        off[1:] = np.cumsum(slots[:-1], dtype=np.uint64)
+    total = int(slots.sum()) if n else 0
+    arena = np.zeros(max(total * 64, 64), dtype=np.uint8)
+    for i, f in enumerate(frames):
+        o = int(off[i]) * 64
+        arena[o:o + len(f)] = np.frombuffer(f, dtype=np.uint8)
+    return arena, off.astype(np.uint32), lens.astype(np.uint16)
+
+
+def tcb_table(rows) -> tuple[np.ndarray, np.ndarray]:
+    """rows: iterable of None (removed slot) or (dport, sport, ipv4_dst_raw, ipv4_src_host,
+    state[, identifier]).  Returns (tcbs TCB_DTYPE, live u8)."""
+    rows = list(rows)
+    t = np.zeros(len(rows), dtype=TCB_DTYPE)
+    live = np.zeros(len(rows), dtype=np.uint8)
+    for i, r in enumerate(rows):
+        if r is None:
+            continue
+        live[i] = 1
+        t[i]["dport"], t[i]["sport"], t[i]["ipv4_dst"], t[i]["ipv4_src"], t[i]["state"] = r[:5]
+        t[i]["identifier"] = r[5] if len(r) > 5 else (i % 65535) + 1
+    return t, live
+
+
+def ip_raw(a: int, b: int, c: int, d: int) -> int:
+    """An IPv4 address as the reference's u32 load of network-order bytes (x86)."""
+    return a | (b << 8) | (c << 16) | (d << 24)
+
+
+def ip_host(a: int, b: int, c: int, d: int) -> int:
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+# -------------------------------------------------------------------------- engine ---
+class DevArray:
+    """A device allocation owned by an Engine."""
+
+    def __init__(self, eng: "Engine", nbytes: int):
+        self.eng, self.nbytes = eng, int(nbytes)
+        p = C.c_void_p()
+        _check(_lib.rxg_dev_alloc(eng.ctx, max(self.nbytes, 1), C.byref(p)), "rxg_dev_alloc")
+        self.ptr = p.value
+
+    def upload(self, a: np.ndarray, stream=None):
+        a = np.ascontiguousarray(a)
+        if a.nbytes > self.nbytes:
+            raise ValueError("upload larger than allocation")
+        _check(_lib.rxg_memcpy_h2d(self.eng.ctx, self.ptr, _ptr(a), a.nbytes, stream), "h2d")
+        _check(_lib.rxg_stream_sync(self.eng.ctx, stream), "sync")
+
+    def download(self, dtype, count, offset_bytes: int = 0, stream=None) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        _check(_lib.rxg_memcpy_d2h(self.eng.ctx, _ptr(out), self.ptr + offset_bytes,
+                                   out.nbytes, stream), "d2h")
+        _check(_lib.rxg_stream_sync(self.eng.ctx, stream), "sync")
+        return out
+
+    def free(self):
+        if self.ptr:
+            _lib.rxg_dev_free(self.eng.ctx, self.ptr)
+            self.ptr = None
+
+
+class Engine:
+    """One rxg context on one GPU (include/rxg.h: rxg_init .. rxg_fini)."""
+
+    def __init__(self, device: int = 0, max_batch: int = 0, max_bytes: int = 0):
+        load_library()
+        cfg = Config(device, max_batch, max_bytes, 0)
+        ctx = C.c_void_p()
+        _check(_lib.rxg_init(C.byref(cfg), C.byref(ctx)), "rxg_init")
+        self.ctx = ctx.value
+        self.device = device
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            _lib.rxg_fini(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def stream(self) -> int:
+        return _lib.rxg_stream(self.ctx)
+
+    def sync(self):
+        _check(_lib.rxg_sync(self.ctx), "rxg_sync")
+
+    def alloc(self, nbytes: int) -> DevArray:
+        return DevArray(self, nbytes)
+
+    def to_device(self, a: np.ndarray) -> DevArray:
+        d = DevArray(self, a.nbytes)
+        d.upload(a)
+        return d
+
+    # --- TCB mirror
+    def tcb_load(self, tcbs: np.ndarray, live: np.ndarray | None = None):
+        tcbs = np.ascontiguousarray(tcbs, dtype=TCB_DTYPE)
+        lv = None if live is None else np.ascontiguousarray(live, dtype=np.uint8)
+        _check(_lib.rxg_tcb_load(self.ctx, _ptr(tcbs), None if lv is None else _ptr(lv),
+                                 len(tcbs)), "rxg_tcb_load")
+
+    def tcb_upsert(self, idx: int, dport: int, sport: int, ipv4_dst: int, ipv4_src: int,
+                   state: int, identifier: int = 0):
+        t = TcbTuple(dport, sport, ipv4_dst, ipv4_src, state, 0, identifier)
+        _check(_lib.rxg_tcb_upsert(self.ctx, idx, C.byref(t)), "rxg_tcb_upsert")
+
+    def tcb_remove(self, idx: int):
+        _check(_lib.rxg_tcb_remove(self.ctx, idx), "rxg_tcb_remove")
+
+    def tcb_set_state(self, idx: int, state: int):
+        _check(_lib.rxg_tcb_set_state(self.ctx, idx, state), "rxg_tcb_set_state")
+
+    def tcb_sync(self):
+        _check(_lib.rxg_tcb_sync(self.ctx), "rxg_tcb_sync")
+
+    def tcb_count(self) -> int:
+        return _lib.rxg_tcb_count(self.ctx)
+
+    # --- bursts
+    def rx_burst_dev(self, frames: int, off64: int, lens: int, n: int, out: int,
+                     rec_kind: int = REC16, stream=None):
+        b = DevBatch(frames, off64, lens, n, rec_kind, out)
+        _check(_lib.rxg_rx_burst_dev(self.ctx, C.byref(b), stream), "rxg_rx_burst_dev")
+
+    def tx_cksum_dev(self, frames: int, off64: int, lens: int, n: int, stream=None):
+        b = DevTxBatch(frames, off64, lens, n, 0)
+        _check(_lib.rxg_tx_cksum_dev(self.ctx, C.byref(b), stream), "rxg_tx_cksum_dev")
+
+    def rx_arena(self, arena: np.ndarray, off64: np.ndarray, lens: np.ndarray,
+                 rec_kind: int = REC48) -> np.ndarray:
+        """Upload a packed arena, run one burst, return the records (numpy)."""
+        n = len(lens)
+        dt = REC48_DTYPE if rec_kind == REC48 else REC16_DTYPE
+        if n == 0:
+            return np.zeros(0, dtype=dt)
+        da, do, dl = self.to_device(arena), self.to_device(off64), self.to_device(lens)
+        dout = self.alloc(n * rec_kind)
+        try:
+            self.rx_burst_dev(da.ptr, do.ptr, dl.ptr, n, dout.ptr, rec_kind)
+            self.sync()
+            return dout.download(dt, n)
+        finally:
+            for d in (da, do, dl, dout):
+                d.free()
+
+    def tx_arena(self, arena: np.ndarray, off64: np.ndarray, lens: np.ndarray) -> np.ndarray:
+        """Run the tx checksum-generate kernel over a packed arena; returns the new arena."""
+        n = len(lens)
+        if n == 0:
+            return arena.copy()
+        da, do, dl = self.to_device(arena), self.to_device(off64), self.to_device(lens)
+        try:
+            self.tx_cksum_dev(da.ptr, do.ptr, dl.ptr, n)
+            self.sync()
+            return da.download(np.uint8, arena.size)
+        finally:
+            for d in (da, do, dl):
+                d.free()
+
+    def rx_burst(self, frames: list[bytes], rec_kind: int = REC48) -> np.ndarray:
+        """rxg_rx_burst over host buffers (DPDK-style views into Python bytes)."""
+        n = len(frames)
+        bufs = [C.create_string_buffer(f, len(f) + 1) for f in frames]
+        views = (PktView * max(n, 1))()
+        for i, b in enumerate(bufs):
+            views[i] = PktView(C.addressof(b), 0, len(frames[i]), 0)
+        dt = REC48_DTYPE if rec_kind == REC48 else REC16_DTYPE
+        out = np.zeros(n, dtype=dt)
+        _check(_lib.rxg_rx_burst(self.ctx, views, n, rec_kind, _ptr(out) if n else None),
+               "rxg_rx_burst")
+        return out
+
+    # --- counters
+    def counters_reset(self, stream=None):
+        _check(_lib.rxg_counters_reset(self.ctx, stream), "rxg_counters_reset")
+
+    def counters(self) -> np.ndarray:
+        out = np.zeros(NCOUNTERS, dtype=np.uint64)
+        _check(_lib.rxg_counters_read(self.ctx, _ptr(out)), "rxg_counters_read")
+        return out
+
+    def counters_dev_ptr(self) -> int:
+        return _lib.rxg_counters_dev(self.ctx)
+
+    # --- synthetic traffic
+    def synth(self, n: int, nflows: int, len_a: int = 1500, mix: int = 0,
+              seed: int = 0x5EED, dst_ip_host: int = 0xC0A84E02, dport: int = 80,
+              with_flows: bool = False, stream=None):
+        """Generate n synthetic frames on the device.  Returns a dict of DevArrays."""
+        p = SynthParams(seed, n, nflows, dst_ip_host, dport, mix, len_a if mix == 0 else 0, 0)
+        nbytes = int(_lib.rxg_synth_arena_bytes(C.byref(p)))
+        arena = self.alloc(nbytes)
+        off = self.alloc(n * 4)
+        lens = self.alloc(n * 2)
+        flows = self.alloc(n * 4) if with_flows else None
+        used = C.c_uint64()
+        _check(_lib.rxg_synth_dev(self.ctx, C.byref(p), arena.ptr, nbytes, off.ptr, lens.ptr,
+                                  flows.ptr if flows else None, C.byref(used), stream),
+               "rxg_synth_dev")
+        return {"arena": arena, "off64": off, "len": lens, "flow": flows, "n": n,
+                "arena_bytes": nbytes}
+
+    # --- events
+    def event(self):
+        e = C.c_void_p()
+        _check(_lib.rxg_event_create(self.ctx, C.byref(e)), "rxg_event_create")
+        return e.value
+
+    def record(self, ev, stream=None):
+        _check(_lib.rxg_event_record(self.ctx, ev, stream), "rxg_event_record")
+
+    def elapsed_ms(self, a, b) -> float:
+        ms = C.c_float()
+        _check(_lib.rxg_event_elapsed_ms(self.ctx, a, b, C.byref(ms)), "rxg_event_elapsed_ms")
+        return ms.value
+
+
+def synthetic_tcb_table(nflows: int, dst_raw: int = None, dport: int = 80):
+    """TCB table of SURVEY.md §8(d): slot 0 = LISTENING on dport (socket_bind leaves sport 0,
+    ipv4_dst network order, socket_interface.c:69-85); slot 1+f = ESTABLISHED child of flow f
+    as tcp_listen fills it (tcp_states.c:185-188)."""
+    if dst_raw is None:
+        dst_raw = ip_raw(192, 168, 78, 2)
+    t = np.zeros(nflows + 1, dtype=TCB_DTYPE)
+    t[0] = (dport, 0, dst_raw, 0, LISTENING, 0, 1)
+    f = np.arange(nflows, dtype=np.uint64)
+    t["dport"][1:] = dport
+    t["sport"][1:] = (1024 + f % 64511).astype(np.int32)
+    t["ipv4_dst"][1:] = dst_raw
+    t["ipv4_src"][1:] = ((10 << 24) | (((f >> 16) & 255) << 16) | (((f >> 8) & 255) << 8)
+                         | (f & 255)).astype(np.uint32)
+    t["state"][1:] = TCP_ESTABLISHED
+    t["identifier"][1:] = ((f + 1) % 65535 + 1).astype(np.uint16)
+    return t, np.ones(nflows + 1, dtype=np.uint8)

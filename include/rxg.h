@@ -1,0 +1,350 @@
+/*
+ * rxg.h — C ABI of the MI355X-native receive-path engine ("rxg").
+ *
+ * rxg replaces the per-packet receive stage of rajneshrat/dpdk-tcpipstack:
+ *
+ *   l2fwd_main_loop: for (i < nb_rx) ether_in(pkts[i])      tcp_ip_stack/main.c:396-399
+ *     ether_in   -> switch ether_type                       tcp_ip_stack/etherin.c:12-37
+ *     ip_in      -> ARP learn, proto==6 -> tcp_in           tcp_ip_stack/ip.c:19-42
+ *     tcp_in     -> findtcb, RST verdicts, tcpswitch[state]  tcp_ip_stack/tcp_in.c:32-84
+ *     findtcb    -> two-pass linear 4-tuple / listener scan tcp_ip_stack/tcp_tcb.c:127-173
+ *     calculate_checksum (RFC 1071 byte loop)               tcp_ip_stack/ip.c:44-59
+ *
+ * with one batched, device-resident pass on gfx950 (parse + IPv4 header checksum +
+ * TCP pseudo-header checksum + 4-tuple -> TCB classify), followed by an in-order host
+ * replay that performs exactly the side effects the reference performs
+ * (free_mbuf, send_reset, ARP learn, max_seq_received, AdjustSendWindow,
+ * tcpswitch[state]).
+ *
+ * Conventions
+ *  - Every entry point returns 0 on success or a negative errno-style code
+ *    (-EINVAL, -ENOMEM, -EIO for a HIP runtime error, -ENODEV without a GPU).
+ *    Nothing asserts; nothing falls back to a CPU path.
+ *  - Plain pointers and sizes only.  "dev" pointers are HIP device pointers.
+ *  - A `stream` argument is a hipStream_t passed as void*; NULL = the context's own stream.
+ *  - Field byte orders follow the reference exactly (see rxg_rec48 below).
+ */
+#ifndef RXG_H
+#define RXG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RXG_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------- */
+/* Protocol constants (wire formats; reference names in comments).            */
+/* ------------------------------------------------------------------------- */
+#define RXG_ETHER_TYPE_IPV4 0x0800 /* ETHER_TYPE_IPv4, etherin.c:28 */
+#define RXG_ETHER_TYPE_ARP  0x0806 /* ETHER_TYPE_ARP,  etherin.c:22 */
+#define RXG_IPPROTO_TCP     6      /* IPPROTO_TCP,     ip.c:29      */
+
+/* TCP_FLAGS, tcp_ip_stack/tcp.h:12-21 */
+#define RXG_TCP_FLAG_FIN 0x01
+#define RXG_TCP_FLAG_SYN 0x02
+#define RXG_TCP_FLAG_RST 0x04
+#define RXG_TCP_FLAG_PSH 0x08
+#define RXG_TCP_FLAG_ACK 0x10
+
+/* enum TCP_STATE_, tcp_ip_stack/tcp_states.h:8-17 */
+enum rxg_tcp_state {
+    RXG_TCP_STATE_CLOSED = 0,
+    RXG_LISTENING = 1,
+    RXG_SYN_SENT = 2,
+    RXG_SYN_RECV = 3,
+    RXG_TCP_ESTABLISHED = 4,
+    RXG_TCP_STATE_FIN_1 = 5,
+    RXG_TCP_FIN_2 = 6,
+    RXG_TCP_STATES = 7
+};
+#define RXG_STATE_NONE 0xFF /* no TCB chosen */
+
+/* Fixed offsets the reference uses regardless of IHL (tcp_in.c:42-45). */
+#define RXG_OFF_IP  14
+#define RXG_OFF_TCP 34
+
+/* Reference table capacity (TOTAL_TCBS, tcp_tcb.c:16). rxg itself has no such cap. */
+#define RXG_REF_TOTAL_TCBS 20000
+
+/* ------------------------------------------------------------------------- */
+/* Per-packet result records.                                                 */
+/* ------------------------------------------------------------------------- */
+
+/* What the reference does with the packet (the branch ether_in/ip_in/tcp_in take). */
+enum rxg_verdict {
+    RXG_V_DISPATCH = 0,          /* tcpswitch[state](tcb, tcp, ip, m)   tcp_in.c:65-72     */
+    RXG_V_RST_NOPCB = 1,         /* ++tcpnopcb; free; send_reset        tcp_in.c:47-53     */
+    RXG_V_RST_LISTEN_NONSYN = 2, /* LISTENING && !SYN: free; send_reset tcp_in.c:54-59     */
+    RXG_V_DROP_NONTCP = 3,       /* IPv4, next_proto_id != 6: free      ip.c:36-39         */
+    RXG_V_ARP = 4,               /* arp_in(m); free_mbuf(m)             etherin.c:22-27    */
+    RXG_V_DROP_L2 = 5            /* other ether_type: free_mbuf         etherin.c:33-34    */
+};
+
+/* rxg_rec16.flags bits */
+enum rxg_rec_flag {
+    RXG_F_IP_OK = 0x01,        /* IPv4 and ip_cksum == 0                                     */
+    RXG_F_TCP_OK = 0x02,       /* TCP and tcp_cksum == 0                                     */
+    RXG_F_LISTEN = 0x04,       /* TCB found by findtcb pass 2 (listener on dport)            */
+    RXG_F_REF_NULLSLOT = 0x08, /* pass 2 met a removed (NULL) slot before its answer: the
+                                  reference dereferences NULL there (tcp_tcb.c:160-162);
+                                  rxg skips the slot and reports it                        */
+    RXG_F_TRUNC = 0x10,        /* frame shorter than the 54 bytes the path reads; bytes at
+                                  and beyond data_len are read as zero                      */
+    RXG_F_ARP_LEARN = 0x20     /* reserved: first sighting of src IP (ip.c:30-32)            */
+};
+
+/*
+ * 16-byte compact record: everything the in-order host replay needs that is not a
+ * plain re-read of the (host-resident) frame.
+ */
+typedef struct rxg_rec16 {
+    int32_t tcb_idx;    /* index into tcbs[] chosen by findtcb (tcp_tcb.c:127-173); -1 = NULL */
+    uint16_t ip_cksum;  /* calculate_checksum(frame+14, 20); 0x0000 = header valid             */
+    uint16_t tcp_cksum; /* calculate_checksum(pseudo || frame[34 .. 14+total_length));
+                           pseudo = {src_addr, dst_addr, 0, 6, htons(total_length-20)}
+                           exactly as ip_out builds it (ip.c:109-118); 0x0000 = valid          */
+    uint8_t verdict;    /* enum rxg_verdict                                                     */
+    uint8_t state;      /* tcbs[tcb_idx]->state at classify time, RXG_STATE_NONE if none        */
+    uint8_t tcp_flags;  /* frame byte 47                                                        */
+    uint8_t flags;      /* enum rxg_rec_flag                                                    */
+    int32_t datalen;    /* ntohs(total_length) - (version_ihl&0xf)*4 - (data_off>>4)*4
+                           as the state handlers compute it (tcp_states.c:48-50,103-111)       */
+} rxg_rec16;
+
+/* 48-byte full record: the compact record plus every header field the path extracts. */
+typedef struct rxg_rec48 {
+    rxg_rec16 c;          /* bytes 0..15                                                  */
+    uint16_t ether_type;  /* 16: ntohs(eth->ether_type)                 etherin.c:21        */
+    uint16_t sport;       /* 18: ntohs(tcp->src_port)                   tcp_tcb.c:135       */
+    uint16_t dport;       /* 20: ntohs(tcp->dst_port)                   tcp_tcb.c:134       */
+    uint8_t l4_proto;     /* 22: ip->next_proto_id                      ip.c:28             */
+    uint8_t version_ihl;  /* 23: ip->version_ihl                        tcp_states.c:49     */
+    uint32_t seq;         /* 24: ntohl(tcp->sent_seq)                   tcp_in.c:66         */
+    uint32_t ack;         /* 28: ntohl(tcp->recv_ack)                   tcp_in.c:71         */
+    uint32_t src_ip;      /* 32: ntohl(ip->src_addr), host order        ip.c:30, tcp_tcb.c:155 */
+    uint32_t dst_ip_raw;  /* 36: ip->dst_addr as loaded (network order) tcp_tcb.c:154       */
+    uint8_t data_off;     /* 40: tcp->data_off (raw byte 46)            tcp_states.c:48     */
+    uint8_t src_mac[6];   /* 41: eth->s_addr                            ip.c:31             */
+    uint8_t reserved;     /* 47: 0                                                          */
+} rxg_rec48;
+/* total_length = c.datalen + (version_ihl & 0xf) * 4 + (data_off >> 4) * 4. */
+
+enum rxg_rec_kind { RXG_REC16 = 16, RXG_REC48 = 48 };
+
+/* ------------------------------------------------------------------------- */
+/* Per-GPU counters (merged across GPUs with an RCCL all-reduce, sum, uint64). */
+/* ------------------------------------------------------------------------- */
+enum rxg_counter {
+    RXG_C_RX = 0,           /* frames seen                                            */
+    RXG_C_BYTES,            /* sum of data_len                                        */
+    RXG_C_IPV4,             /* ether_type 0x0800                                      */
+    RXG_C_ARP,              /* ether_type 0x0806                                      */
+    RXG_C_OTHER_L2,         /* any other ether_type                                   */
+    RXG_C_TCP,              /* IPv4 with next_proto_id 6                              */
+    RXG_C_NON_TCP,          /* IPv4, other protocol                                   */
+    RXG_C_IP_CKSUM_BAD,     /* IPv4 with ip_cksum != 0                                */
+    RXG_C_TCP_CKSUM_BAD,    /* TCP with tcp_cksum != 0 (tcpchecksumerror, tcp_in.c:18) */
+    RXG_C_TCB_HIT_EXACT,    /* findtcb pass 1 hit                                     */
+    RXG_C_TCB_HIT_LISTEN,   /* findtcb pass 2 hit                                     */
+    RXG_C_NOPCB,            /* findtcb NULL (tcpnopcb, tcp_in.c:48)                   */
+    RXG_C_LISTEN_NONSYN,    /* RST to a non-SYN on a listener                         */
+    RXG_C_DISPATCH,         /* handed to tcpswitch[state]                             */
+    RXG_C_REF_NULLSLOT,     /* reference would have dereferenced a NULL slot          */
+    RXG_C_TRUNC,            /* frames shorter than 54 bytes                           */
+    RXG_NCOUNTERS
+};
+
+/* ------------------------------------------------------------------------- */
+/* Context                                                                    */
+/* ------------------------------------------------------------------------- */
+typedef struct rxg_ctx rxg_ctx;
+
+typedef struct rxg_config {
+    int32_t device;        /* HIP device ordinal (one context per GPU, one rx thread each) */
+    uint32_t max_batch;    /* largest n passed to the host-buffer entry points (staging)   */
+    uint32_t max_bytes;    /* staging arena bytes for host-buffer entry points            */
+    uint32_t flags;        /* reserved, 0                                                  */
+} rxg_config;
+
+int rxg_abi_version(void);
+const char *rxg_build_info(void);
+int rxg_init(const rxg_config *cfg, rxg_ctx **out);
+int rxg_fini(rxg_ctx *ctx);
+/* Block until all work queued on the context's stream is done. */
+int rxg_sync(rxg_ctx *ctx);
+/* The hipStream_t rxg launches on when a NULL stream is passed. */
+void *rxg_stream(rxg_ctx *ctx);
+
+/* ------------------------------------------------------------------------- */
+/* TCB mirror.  The reference mutates `tcbs[]` directly (tcp_tcb.c:21-22,     */
+/* alloc_tcb :34-106, remove_tcb :175-186, tuple writes in socket_interface.c */
+/* :80-83,:329-332 and tcp_states.c :25-27,:185-188).  A caller mirrors each   */
+/* such write with one of these calls; they are applied to the device copy   */
+/* before the next burst.                                                     */
+/* ------------------------------------------------------------------------- */
+typedef struct rxg_tcb_tuple {
+    int32_t dport;       /* struct tcb::dport (host order, int)          tcp_tcb.h:17 */
+    int32_t sport;       /* struct tcb::sport (host order, int)          tcp_tcb.h:18 */
+    uint32_t ipv4_dst;   /* struct tcb::ipv4_dst, compared RAW to ip->dst_addr        */
+    uint32_t ipv4_src;   /* struct tcb::ipv4_src, compared to ntohl(ip->src_addr)     */
+    uint8_t state;       /* struct tcb::state (enum rxg_tcp_state)                    */
+    uint8_t pad;
+    uint16_t identifier; /* struct tcb::identifier (1..65535 cyclic)                  */
+} rxg_tcb_tuple;
+
+/* tcbs[idx] = tuple (a live slot).  idx >= current Ntcb grows Ntcb to idx+1; slots in
+   between are NULL, as if allocated and removed. */
+int rxg_tcb_upsert(rxg_ctx *ctx, int32_t idx, const rxg_tcb_tuple *t);
+/* tcbs[idx] = NULL (remove_tcb).  Ntcb never shrinks (tcp_tcb.c:175-186). */
+int rxg_tcb_remove(rxg_ctx *ctx, int32_t idx);
+/* tcbs[idx]->state = state. */
+int rxg_tcb_set_state(rxg_ctx *ctx, int32_t idx, uint8_t state);
+/* Replace the whole table: tcbs[0..ntcb), live[i]==0 marks a NULL slot. */
+int rxg_tcb_load(rxg_ctx *ctx, const rxg_tcb_tuple *tcbs, const uint8_t *live, int32_t ntcb);
+/* Push pending mirror changes to the device (done implicitly by every burst). */
+int rxg_tcb_sync(rxg_ctx *ctx);
+/* Current Ntcb of the mirror. */
+int32_t rxg_tcb_count(rxg_ctx *ctx);
+
+/* ------------------------------------------------------------------------- */
+/* Receive burst: parse + checksum + classify.  Pure: no frees, no side       */
+/* effects, counters only.                                                    */
+/* ------------------------------------------------------------------------- */
+
+/* Device-resident batch.  Frame i occupies bytes [frames + 64*off64[i],
+   + len[i]); the bytes up to the next 64-byte boundary must be readable
+   (their contents are ignored).  len[i] = rte_pktmbuf_data_len(m). */
+typedef struct rxg_dev_batch {
+    const void *frames;     /* dev */
+    const uint32_t *off64;  /* dev, n entries, in 64-byte units */
+    const uint16_t *len;    /* dev, n entries */
+    uint32_t n;
+    uint32_t rec_kind;      /* RXG_REC16 or RXG_REC48 */
+    void *out;              /* dev, n records of rec_kind bytes */
+} rxg_dev_batch;
+
+/* Replaces the per-packet loop over ether_in() (main.c:396-399) for a batch already
+   resident in HBM.  Asynchronous on `stream`. */
+int rxg_rx_burst_dev(rxg_ctx *ctx, const rxg_dev_batch *b, void *stream);
+
+/* DPDK-compatible host packet view: frame = (char*)buf_addr + data_off, data_len bytes
+   (struct rte_mbuf fields of the same names). */
+typedef struct rxg_pkt_view {
+    const void *buf_addr;
+    uint16_t data_off;
+    uint16_t data_len;
+    uint32_t pad;
+} rxg_pkt_view;
+
+/* Host-buffer burst: packs the frames into pinned staging, H2D, kernel, D2H into
+   `out_host` (n records of rec_kind bytes).  Synchronous. */
+int rxg_rx_burst(rxg_ctx *ctx, const rxg_pkt_view *pkts, uint32_t n, uint32_t rec_kind,
+                 void *out_host);
+
+/* ------------------------------------------------------------------------- */
+/* Transmit checksum generate: what ip_out computes (ip.c:97-118) for a batch  */
+/* of frames whose Ethernet/IPv4/TCP headers the host has filled.  Writes      */
+/* hdr_checksum (frame bytes 24-25) and tcp cksum (bytes 50-51) in place, both */
+/* stored htons(calculate_checksum(..)) with the field zeroed while summing.   */
+/* The TCP span is pseudo || frame[34 .. 14+total_length).                     */
+/* ------------------------------------------------------------------------- */
+typedef struct rxg_dev_tx_batch {
+    void *frames;           /* dev, modified in place */
+    const uint32_t *off64;  /* dev */
+    const uint16_t *len;    /* dev */
+    uint32_t n;
+    uint32_t pad;
+} rxg_dev_tx_batch;
+int rxg_tx_cksum_dev(rxg_ctx *ctx, const rxg_dev_tx_batch *b, void *stream);
+
+/* ------------------------------------------------------------------------- */
+/* Counters                                                                   */
+/* ------------------------------------------------------------------------- */
+int rxg_counters_reset(rxg_ctx *ctx, void *stream);
+/* Synchronous read of the RXG_NCOUNTERS uint64 counters. */
+int rxg_counters_read(rxg_ctx *ctx, uint64_t *out);
+/* Device address of the uint64[RXG_NCOUNTERS] counter block (for an in-place
+   RCCL all-reduce by the caller). */
+void *rxg_counters_dev(rxg_ctx *ctx);
+
+/* ------------------------------------------------------------------------- */
+/* In-order hand-off (the side effects of etherin.c:21-35, ip.c:28-39,        */
+/* tcp_in.c:47-72).  The caller supplies the reference's own functions.       */
+/* ------------------------------------------------------------------------- */
+typedef struct rxg_handoff_ops {
+    void *user;
+    void (*free_mbuf)(void *user, void *mbuf);                               /* main.c:206   */
+    int (*arp_in)(void *user, void *mbuf);                                   /* arp.c:113    */
+    /* ip.c:30-32: if (!get_mac(src)) add_mac(src, mac) */
+    int (*get_mac)(void *user, uint32_t ipv4_host, unsigned char *mac_out);  /* arp.c:215    */
+    int (*add_mac)(void *user, uint32_t ipv4_host, const unsigned char *mac);/* arp.c:282    */
+    void (*send_reset)(void *user, void *ip_hdr, void *tcp_hdr);             /* tcp_out.c:103*/
+    /* tcp_in.c:66-68 + 71: max_seq_received update and AdjustSendWindow(tcb, ack) */
+    void (*on_segment)(void *user, int32_t tcb_idx, uint32_t seq, uint32_t ack);
+    /* tcpswitch[state](tcb, tcp_hdr, ip_hdr, mbuf)             tcp_states.c:257-265 */
+    int (*tcpswitch)(void *user, int32_t tcb_idx, uint8_t state, void *tcp_hdr, void *ip_hdr,
+                     void *mbuf);
+} rxg_handoff_ops;
+
+/* Performs, in packet order, the side effects ether_in() would have performed for
+   pkts[0..n) given their records.  frames[i] = the frame bytes of mbufs[i].  The
+   composition rxg_rx_burst + rxg_rx_replay equals `for (i<n) ether_in(mbufs[i])` when
+   no handler in the batch mutates the TCB table; handlers that do must mirror their
+   writes with rxg_tcb_* (see INTEGRATION.md). */
+int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
+                  void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic traffic (bench / tests): Eth + IPv4 (IHL 5) + TCP (doff 5, ACK)   */
+/* frames with valid checksums, SURVEY.md §8(d).                               */
+/* ------------------------------------------------------------------------- */
+typedef struct rxg_synth_params {
+    uint64_t seed;        /* payload / header PRNG seed                          */
+    uint32_t n;           /* frames                                              */
+    uint32_t nflows;      /* flow f: src 10.(f>>16).(f>>8).(f), sport 1024+f%64511 */
+    uint32_t dst_ip_host; /* 192.168.78.2 = 0xC0A84E02 (config.h:8)             */
+    uint16_t dport;       /* 80                                                  */
+    uint16_t mix;         /* 0: all frames len_a; 1: IMIX 64/576/1500 at 7:4:1    */
+    uint16_t len_a;       /* frame length when mix == 0                          */
+    uint16_t pad;
+} rxg_synth_params;
+
+/* Fills off64/len (dev) and frames (dev) for p->n frames, packed at 64-byte aligned
+   starts; returns the arena bytes used in *arena_bytes.  Frame flows are uniform over
+   nflows (stored per frame in flow_out, dev, may be NULL). */
+int rxg_synth_dev(rxg_ctx *ctx, const rxg_synth_params *p, void *frames, uint64_t frames_cap,
+                  uint32_t *off64, uint16_t *len, uint32_t *flow_out, uint64_t *arena_bytes,
+                  void *stream);
+/* Host helper: the arena bytes rxg_synth_dev needs for p. */
+uint64_t rxg_synth_arena_bytes(const rxg_synth_params *p);
+
+/* ------------------------------------------------------------------------- */
+/* Device memory helpers (so ctypes/C callers need no other HIP binding).      */
+/* ------------------------------------------------------------------------- */
+int rxg_dev_alloc(rxg_ctx *ctx, uint64_t bytes, void **out);
+int rxg_dev_free(rxg_ctx *ctx, void *p);
+int rxg_host_alloc_pinned(rxg_ctx *ctx, uint64_t bytes, void **out);
+int rxg_host_free_pinned(rxg_ctx *ctx, void *p);
+int rxg_memcpy_h2d(rxg_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
+int rxg_memcpy_d2h(rxg_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
+int rxg_memset_dev(rxg_ctx *ctx, void *dst, int value, uint64_t bytes, void *stream);
+int rxg_stream_sync(rxg_ctx *ctx, void *stream);
+
+/* Event timing on a stream (bench): returns ms between two recorded events. */
+typedef struct rxg_event rxg_event;
+int rxg_event_create(rxg_ctx *ctx, rxg_event **out);
+int rxg_event_record(rxg_ctx *ctx, rxg_event *e, void *stream);
+int rxg_event_elapsed_ms(rxg_ctx *ctx, rxg_event *a, rxg_event *b, float *ms);
+int rxg_event_destroy(rxg_ctx *ctx, rxg_event *e);
+
+/* Last error text of this thread (static storage). */
+const char *rxg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RXG_H */

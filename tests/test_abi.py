@@ -1,0 +1,108 @@
+"""CPU tests of the drop-in boundary: librxg.so loads and exports every entry point that
+include/rxg.h declares; the Python mirror's constants and layouts match the header."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import rxg
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rxg.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rxg_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ["rxg_init", "rxg_fini", "rxg_rx_burst_dev", "rxg_rx_burst", "rxg_rx_replay",
+                 "rxg_tcb_upsert", "rxg_tcb_remove", "rxg_tcb_set_state", "rxg_tx_cksum_dev",
+                 "rxg_counters_read", "rxg_counters_dev"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = rxg.load_library()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", rxg.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (rxg_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_has_gfx950_code_object():
+    data = open(rxg.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_abi_version_and_build_info():
+    lib = rxg.load_library()
+    assert lib.rxg_abi_version() == 1
+    assert b"gfx950" in lib.rxg_build_info()
+
+
+def test_struct_layouts_match_header():
+    hdr = open(HEADER).read()
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "rxg.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %d\n", sizeof(rxg_rec16), sizeof(rxg_rec48),
+         sizeof(rxg_tcb_tuple), sizeof(rxg_dev_batch), sizeof(rxg_pkt_view),
+         sizeof(rxg_synth_params), offsetof(rxg_rec48, src_mac), RXG_NCOUNTERS);
+  return 0;
+}'''
+    tmp = os.path.join(ROOT, "build_abi_probe")
+    os.makedirs(tmp, exist_ok=True)
+    with open(os.path.join(tmp, "p.c"), "w") as fh:
+        fh.write(src)
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), os.path.join(tmp, "p.c"), "-o",
+                    os.path.join(tmp, "p")], check=True)
+    got = subprocess.run([os.path.join(tmp, "p")], capture_output=True, text=True).stdout.split()
+    assert [int(x) for x in got] == [16, 48, 20, C.sizeof(rxg.DevBatch), C.sizeof(rxg.PktView),
+                                     C.sizeof(rxg.SynthParams), 41, rxg.NCOUNTERS]
+    assert rxg.REC48_DTYPE.fields["src_mac"][1] == 41
+    assert "RXG_NCOUNTERS" in hdr
+
+
+def test_python_constants_match_header():
+    hdr = open(HEADER).read()
+    enum = re.search(r"enum rxg_counter \{(.*?)\};", hdr, re.S).group(1)
+    names = [m.lower()[6:] for m in re.findall(r"\b(RXG_C_[A-Z0-9_]+)", enum)]
+    assert names == rxg.COUNTERS
+    for name, val in [("RXG_V_DISPATCH", 0), ("RXG_V_RST_NOPCB", 1), ("RXG_V_RST_LISTEN_NONSYN", 2),
+                      ("RXG_V_DROP_NONTCP", 3), ("RXG_V_ARP", 4), ("RXG_V_DROP_L2", 5)]:
+        assert re.search(rf"{name} = {val}\b", hdr)
+
+
+def test_no_gpu_fails_loudly():
+    """Without a GPU the engine refuses to run (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(rxg.RxgError, match="rxg_init"):
+        rxg.Engine(0)
+
+
+def test_product_does_not_link_the_oracle():
+    out = subprocess.run(["readelf", "-d", rxg.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert "oracle" not in out
+    syms = subprocess.run(["nm", "-D", rxg.LIB_PATH], capture_output=True, text=True).stdout
+    assert "orc_" not in syms
+
+
+def test_pack_arena_layout():
+    frames = [b"a" * 10, b"b" * 64, b"c" * 65, b""]
+    arena, off, lens = rxg.pack_arena(frames)
+    assert off.tolist() == [0, 1, 2, 4] and lens.tolist() == [10, 64, 65, 0]
+    assert arena.size == 4 * 64 and bytes(arena[128:193]) == b"c" * 65
