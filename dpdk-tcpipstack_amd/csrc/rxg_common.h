@@ -17,14 +17,18 @@ namespace rxg {
 //   bucket table: nbuckets x 4 slots x 16 B = one 64-byte line per bucket.  A slot is
 //     {ports = dport<<16 | sport, ipv4_dst raw, ipv4_src host, value}; value = the
 //     LOWEST tcbs[] index holding that exact tuple (findtcb pass 1 returns the first
-//     match, tcp_tcb.c:145-159), or kEmpty.  Linear probing over buckets.
+//     match, tcp_tcb.c:145-159) in bits 0..23 and that TCB's state (tcp_in.c:54 reads it
+//     after the lookup) in bits 24..31; kEmpty marks a free slot.  Linear probing over
+//     buckets; a lookup ends at the first bucket holding a free slot.
 //   listen[65536]: lowest index i with tcbs[i] live, LISTENING, dport == port (pass 2,
-//     tcp_tcb.c:160-169), or -1.
-//   state[ntcb]: tcbs[i]->state (tcp_in.c:54 reads it after the lookup).
+//     tcp_tcb.c:160-169), or -1.  Its state is LISTENING by construction.
 //   min_null: lowest removed slot index (pass 2 would dereference NULL there).
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr int kSlotsPerBucket = 4;
+constexpr uint32_t kIdxMask = 0x00FFFFFFu;
+constexpr int kStateShift = 24;
+constexpr int32_t kMaxTcbs = 0x00FFFFFF;  // indices 0 .. kMaxTcbs-1
 
 RXG_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
@@ -81,7 +85,6 @@ RXG_HD uint32_t imix_len(int pos)
 struct DevTable {
     const uint4 *buckets;  // nbuckets * 4 slots
     const int32_t *listen; // 65536
-    const uint8_t *state;  // ntcb
     uint32_t bucket_mask;  // nbuckets - 1
     int32_t ntcb;
     int32_t min_null;      // INT32_MAX if none

@@ -57,7 +57,10 @@ struct DevBuf {
 struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    uint32_t max_blocks = 2048;
+    uint32_t max_blocks = 2048;     // RXG_MAX_BLOCKS overrides the occupancy-derived grid
+    uint32_t grid_rec16 = 0, grid_rec48 = 0, grid_tx = 0;
+    int variant = 0;  // RXG_VARIANT: experiment kernels (tools/kbench only)
+    int nocount = 0;  // RXG_NOCOUNT: experiment only, skip the counter reduction
 
     // host mirror of tcbs[0..ntcb)
     std::vector<rxg_tcb_tuple> tcb;
@@ -65,7 +68,7 @@ struct rxg_ctx {
     bool dirty = true;
 
     // device mirror
-    DevBuf buckets, listen, state;
+    DevBuf buckets, listen;
     uint32_t bucket_mask = 0;
     int32_t dev_ntcb = 0;
     int32_t dev_min_null = INT32_MAX;
@@ -83,6 +86,8 @@ struct rxg_ctx {
     uint16_t *d_len = nullptr;
     uint8_t *d_out = nullptr;
 };
+
+static constexpr size_t kCounterBytes = (size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS * sizeof(uint64_t);
 
 struct rxg_event {
     hipEvent_t e;
@@ -106,11 +111,7 @@ extern "C" int rxg_abi_version(void) { return RXG_ABI_VERSION; }
 
 extern "C" const char *rxg_build_info(void)
 {
-    return "rxg " __DATE__ " gfx950"
-#if RXG_NT_LOADS
-           " nt-loads"
-#endif
-        ;
+    return "rxg " __DATE__ " gfx950";
 }
 
 extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
@@ -131,17 +132,22 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     if (rc) { delete c; return rc; }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) {
-        // persistent grid: 8 workgroups of 256 threads per CU
-        c->max_blocks = (uint32_t)prop.multiProcessorCount * 8u;
+        // one generation of resident workgroups per CU (grid-stride over slices)
+        const uint32_t cus = (uint32_t)prop.multiProcessorCount;
+        c->grid_rec16 = cus * (uint32_t)rx_blocks_per_cu(16);
+        c->grid_rec48 = cus * (uint32_t)rx_blocks_per_cu(48);
+        c->grid_tx = cus * (uint32_t)rx_blocks_per_cu(0);
+        c->max_blocks = 0;
         if (const char *g = getenv("RXG_MAX_BLOCKS")) c->max_blocks = (uint32_t)atoi(g);
-        if (c->max_blocks == 0) c->max_blocks = 2048;
     }
+    if (const char *v = getenv("RXG_VARIANT")) c->variant = atoi(v);
+    if (const char *v = getenv("RXG_NOCOUNT")) c->nocount = atoi(v);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(-EIO, "rxg_init: hipStreamCreate failed");
     }
-    if (hipMalloc(&c->counters, RXG_NCOUNTERS * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->counters, 0, RXG_NCOUNTERS * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&c->counters, kCounterBytes) != hipSuccess ||
+        hipMemset(c->counters, 0, kCounterBytes) != hipSuccess) {
         rxg_fini(c);
         return fail(-ENOMEM, "rxg_init: counters");
     }
@@ -171,7 +177,7 @@ extern "C" int rxg_fini(rxg_ctx *c)
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->buckets, &c->listen, &c->state})
+    for (DevBuf *b : {&c->buckets, &c->listen})
         if (b->p) (void)hipFree(b->p);
     if (c->counters) (void)hipFree(c->counters);
     if (c->h_arena) (void)hipHostFree(c->h_arena);
@@ -200,7 +206,7 @@ static hipStream_t pick(rxg_ctx *c, void *s) { return s ? (hipStream_t)s : c->st
 // -------------------------------------------------------------------- TCB mirror ---
 static int grow_to(rxg_ctx *c, int32_t idx)
 {
-    if (idx < 0) return fail(-EINVAL, "tcb index %d < 0", idx);
+    if (idx < 0 || idx >= kMaxTcbs) return fail(-EINVAL, "tcb index %d outside 0..%d", idx, kMaxTcbs - 1);
     if ((size_t)idx >= c->tcb.size()) {
         c->tcb.resize((size_t)idx + 1, rxg_tcb_tuple{});
         c->live.resize((size_t)idx + 1, 0);
@@ -211,6 +217,7 @@ static int grow_to(rxg_ctx *c, int32_t idx)
 extern "C" int rxg_tcb_upsert(rxg_ctx *c, int32_t idx, const rxg_tcb_tuple *t)
 {
     if (!c || !t) return fail(-EINVAL, "rxg_tcb_upsert: NULL argument");
+    if (t->state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_upsert: state %u", t->state);
     int rc = grow_to(c, idx);
     if (rc) return rc;
     c->tcb[idx] = *t;
@@ -232,6 +239,7 @@ extern "C" int rxg_tcb_remove(rxg_ctx *c, int32_t idx)
 extern "C" int rxg_tcb_set_state(rxg_ctx *c, int32_t idx, uint8_t state)
 {
     if (!c) return fail(-EINVAL, "rxg_tcb_set_state: ctx NULL");
+    if (state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_set_state: state %u", state);
     if (idx < 0 || (size_t)idx >= c->tcb.size() || !c->live[idx])
         return fail(-EINVAL, "rxg_tcb_set_state: index %d is not a live slot", idx);
     c->tcb[idx].state = state;
@@ -242,6 +250,10 @@ extern "C" int rxg_tcb_set_state(rxg_ctx *c, int32_t idx, uint8_t state)
 extern "C" int rxg_tcb_load(rxg_ctx *c, const rxg_tcb_tuple *tcbs, const uint8_t *live, int32_t ntcb)
 {
     if (!c || ntcb < 0 || (ntcb > 0 && !tcbs)) return fail(-EINVAL, "rxg_tcb_load: bad arguments");
+    if (ntcb > kMaxTcbs) return fail(-EINVAL, "rxg_tcb_load: %d TCBs exceed %d", ntcb, kMaxTcbs);
+    for (int32_t i = 0; i < ntcb; ++i)
+        if ((!live || live[i]) && tcbs[i].state >= RXG_TCP_STATES)
+            return fail(-EINVAL, "rxg_tcb_load: slot %d state %u", i, tcbs[i].state);
     c->tcb.assign(tcbs, tcbs + ntcb);
     if (live)
         c->live.assign(live, live + ntcb);
@@ -275,7 +287,6 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
     std::unordered_map<Key, int32_t, KeyHash> first;
     first.reserve((size_t)n * 2 + 1);
     std::vector<int32_t> listen(65536, -1);
-    std::vector<uint8_t> state((size_t)std::max(n, 1), RXG_STATE_NONE);
     int32_t min_null = INT32_MAX;
     for (int32_t i = 0; i < n; ++i) {
         if (!c->live[i]) {
@@ -283,7 +294,6 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
             continue;
         }
         const rxg_tcb_tuple &t = c->tcb[i];
-        state[i] = t.state;
         // a tuple whose int ports are outside 0..65535 can never equal a packet's u16 port
         if (port_ok(t.dport) && port_ok(t.sport)) {
             Key k{((uint32_t)t.dport << 16) | (uint32_t)t.sport, t.ipv4_dst, t.ipv4_src};
@@ -306,7 +316,7 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
                     e[0] = kv.first.ports;
                     e[1] = kv.first.dst;
                     e[2] = kv.first.src;
-                    e[3] = (uint32_t)kv.second;
+                    e[3] = (uint32_t)kv.second | ((uint32_t)c->tcb[kv.second].state << kStateShift);
                     placed = 1;
                 }
             }
@@ -316,10 +326,8 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
     }
     if ((rc = ensure(c->buckets, slots.size() * 4))) return rc;
     if ((rc = ensure(c->listen, listen.size() * 4))) return rc;
-    if ((rc = ensure(c->state, state.size()))) return rc;
     HIP_OK(hipMemcpyAsync(c->buckets.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipMemcpyAsync(c->listen.p, listen.data(), listen.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(c->state.p, state.data(), state.size(), hipMemcpyHostToDevice, c->stream));
     // the host vectors die here: the copies must have consumed them
     HIP_OK(hipStreamSynchronize(c->stream));
     c->bucket_mask = nb - 1;
@@ -334,7 +342,6 @@ static DevTable table_view(const rxg_ctx *c)
     DevTable t;
     t.buckets = (const uint4 *)c->buckets.p;
     t.listen = (const int32_t *)c->listen.p;
-    t.state = (const uint8_t *)c->state.p;
     t.bucket_mask = c->bucket_mask;
     t.ntcb = c->dev_ntcb;
     t.min_null = c->dev_min_null;
@@ -361,8 +368,10 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
     L.mode = (int)b->rec_kind;
     L.out = (uint8_t *)b->out;
     L.table = table_view(c);
-    L.counters = c->counters;
-    L.max_blocks = c->max_blocks;
+    L.counters = c->nocount ? nullptr : c->counters;
+    L.max_blocks = c->max_blocks ? c->max_blocks : (b->rec_kind == RXG_REC48 ? c->grid_rec48 : c->grid_rec16);
+    if (L.max_blocks == 0) L.max_blocks = 1024;
+    L.variant = c->variant;
     HIP_OK(launch_rx(L, pick(c, stream)));
     return 0;
 }
@@ -383,7 +392,8 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
     L.mode = 0;
     L.out = nullptr;
     L.counters = nullptr;
-    L.max_blocks = c->max_blocks;
+    L.max_blocks = c->max_blocks ? c->max_blocks : c->grid_tx;
+    if (L.max_blocks == 0) L.max_blocks = 1024;
     HIP_OK(launch_rx(L, pick(c, stream)));
     return 0;
 }
@@ -432,7 +442,7 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
 extern "C" int rxg_counters_reset(rxg_ctx *c, void *stream)
 {
     if (!c) return fail(-EINVAL, "rxg_counters_reset: ctx NULL");
-    HIP_OK(hipMemsetAsync(c->counters, 0, RXG_NCOUNTERS * sizeof(unsigned long long), pick(c, stream)));
+    HIP_OK(hipMemsetAsync(c->counters, 0, kCounterBytes, pick(c, stream)));
     return 0;
 }
 
@@ -440,7 +450,13 @@ extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
 {
     if (!c || !out) return fail(-EINVAL, "rxg_counters_read: NULL argument");
     HIP_OK(hipStreamSynchronize(c->stream));
-    HIP_OK(hipMemcpy(out, c->counters, RXG_NCOUNTERS * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    std::vector<uint64_t> rows((size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS);
+    HIP_OK(hipMemcpy(rows.data(), c->counters, kCounterBytes, hipMemcpyDeviceToHost));
+    for (int k = 0; k < RXG_NCOUNTERS; ++k) {
+        uint64_t v = 0;
+        for (int r = 0; r < RXG_COUNTER_ROWS; ++r) v += rows[(size_t)r * RXG_NCOUNTERS + k];
+        out[k] = v;
+    }
     return 0;
 }
 

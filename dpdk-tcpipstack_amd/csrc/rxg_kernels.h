@@ -15,7 +15,8 @@ struct LaunchRx {
     uint8_t *out;
     DevTable table;
     unsigned long long *counters;
-    uint32_t max_blocks;   // persistent grid cap (grid-stride over 64-frame slices)
+    uint32_t max_blocks;   // grid cap (grid-stride over 64-frame slices)
+    int variant;           // 0 = production kernel; >0 = experiment variants (RXG_VARIANT)
 };
 
 struct LaunchSynth {
@@ -29,6 +30,8 @@ struct LaunchSynth {
 };
 
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
+// resident 256-thread workgroups per CU of the production kernel of `mode`
+int rx_blocks_per_cu(int mode);
 hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);
 
 }  // namespace rxg

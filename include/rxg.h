@@ -265,10 +265,13 @@ int rxg_tx_cksum_dev(rxg_ctx *ctx, const rxg_dev_tx_batch *b, void *stream);
 /* Counters                                                                   */
 /* ------------------------------------------------------------------------- */
 int rxg_counters_reset(rxg_ctx *ctx, void *stream);
-/* Synchronous read of the RXG_NCOUNTERS uint64 counters. */
+/* Synchronous read of the RXG_NCOUNTERS uint64 counters (the replica rows summed). */
 int rxg_counters_read(rxg_ctx *ctx, uint64_t *out);
-/* Device address of the uint64[RXG_NCOUNTERS] counter block (for an in-place
-   RCCL all-reduce by the caller). */
+/* The device keeps RXG_COUNTER_ROWS replicas of the counter block so that workgroups do
+   not all add to one cache line; counter k = sum over rows r of block[r][k]. */
+#define RXG_COUNTER_ROWS 64
+/* Device address of the uint64[RXG_COUNTER_ROWS][RXG_NCOUNTERS] block: an in-place RCCL
+   all-reduce (sum) over it followed by rxg_counters_read merges counters across GPUs. */
 void *rxg_counters_dev(rxg_ctx *ctx);
 
 /* ------------------------------------------------------------------------- */

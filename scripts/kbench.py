@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmark: interleaved rounds of kernel variants in ONE process
+(cdna_hip_programming.md §5.4 rule 24).  Variants are (RXG_VARIANT, RXG_MAX_BLOCKS) pairs;
+each gets its own rxg context; all share the same device-resident workloads.
+
+  python scripts/kbench.py --variants 0:2048,2:2048 --workloads c3,c2 --rounds 5
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch  # noqa: F401  (one HIP runtime per process)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")]
+import rxg  # noqa: E402
+
+WL = {"c3": (1500, 1000, 0, 1), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0:2048")
+    ap.add_argument("--workloads", default="c3,c2")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--rec", type=int, default=16)
+    args = ap.parse_args()
+
+    base = rxg.Engine(0)
+    wls = {}
+    for w in args.workloads.split(","):
+        L, flows, mix, copies = WL[w]
+        bs = [base.synth(n=args.frames, nflows=flows, len_a=L or 1500, mix=mix, seed=77 + c)
+              for c in range(copies)]
+        lens = bs[0]["len"].download(np.uint16, args.frames)
+        tcb, live = rxg.synthetic_tcb_table(flows)
+        wls[w] = (bs, int(lens.astype(np.uint64).sum()), tcb, live)
+    out = base.alloc(args.frames * args.rec)
+    base.sync()
+
+    engines = {}
+    for v in args.variants.split(","):
+        parts = v.split(":")
+        os.environ["RXG_VARIANT"] = parts[0]
+        os.environ["RXG_MAX_BLOCKS"] = parts[1]
+        os.environ["RXG_NOCOUNT"] = "1" if (len(parts) > 2 and parts[2] == "nc") else "0"
+        engines[v] = rxg.Engine(0)
+    res = {(v, w): [] for v in engines for w in wls}
+    for r in range(args.rounds):
+        for w, (bs, nbytes, tcb, live) in wls.items():
+            for v, eng in engines.items():
+                eng.tcb_load(tcb, live)
+                eng.tcb_sync()
+                evs = [(eng.event(), eng.event()) for _ in range(args.iters)]
+                for i in range(2):
+                    b = bs[i % len(bs)]
+                    eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, args.frames, out.ptr, args.rec)
+                for i in range(args.iters):
+                    b = bs[(i + 2) % len(bs)]
+                    eng.record(evs[i][0])
+                    eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, args.frames, out.ptr, args.rec)
+                    eng.record(evs[i][1])
+                eng.sync()
+                ms = [eng.elapsed_ms(a, b) for a, b in evs]
+                res[(v, w)].append(float(np.median(ms)))
+                for a, b in evs:
+                    rxg.load_library().rxg_event_destroy(eng.ctx, a)
+                    rxg.load_library().rxg_event_destroy(eng.ctx, b)
+    for (v, w), ms in res.items():
+        nbytes = wls[w][1]
+        med = float(np.median(ms))
+        print(json.dumps({"variant": v, "workload": w, "kernel_us_median": round(med * 1e3, 2),
+                          "kernel_us_min": round(min(ms) * 1e3, 2),
+                          "GBps": round(nbytes / (med * 1e-3) / 1e9, 1),
+                          "frac_8TBs": round(nbytes / (med * 1e-3) / 8e12, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
