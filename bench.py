@@ -32,6 +32,9 @@ import rxg  # noqa: E402  (after torch: one HIP runtime per process)
 
 METRIC = "Mpps + GB/s rx parse+checksum+classify, device-resident, 64B & 1500B frames"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Per-launch HBM traffic from the committed rocprofv3 PMC passes of this same command
+# (scripts/gpu_check.sh pmc; scripts/pmc_traffic.py applies the gfx950 FETCH_SIZE x2 fix).
+TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r01/c3/traffic.json"}
 WORKLOADS = {
     # name: (frame_len, flows, mix, rotating copies)
     "c3_1500B_1Kflows": (1500, 1000, 0, 1),
@@ -235,6 +238,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds)
 
+    traffic, traffic_src = None, None
+    tf = TRAFFIC_FILES.get((args.workload, wl.n, args.rec))
+    if tf and os.path.exists(os.path.join(ROOT, tf)):
+        with open(os.path.join(ROOT, tf)) as fh:
+            traffic = json.load(fh)["hbm_bytes_per_launch"]
+        traffic_src = tf
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -258,7 +268,8 @@ def main():
                        "parallelism": f"dp{world} (independent batches, replicated TCB mirror)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None,
+                         "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel_us": round(k_avg_s * 1e6, 2),
                          "algorithmic_bytes_per_launch": wl.bytes_per_batch},
             "cpu_baseline": cpu,
