@@ -126,6 +126,115 @@ def time_workload(eng, wl, steps, warmup, device, stream):
     return elapsed, kern_ms
 
 
+def copy_inclusive_leg(eng, wl, steps, warmup, device):
+    """The path as it runs from host mbufs: pinned H2D of the packed batch (arena +
+    descriptors), the rx kernel, D2H of the records; one stream, back to back.  PCIe-bound;
+    reported beside `value`, never as it."""
+    b = wl.batches[0]
+    nb = b["arena_bytes"]
+    h_arena, h_off, h_len = eng.pinned(nb), eng.pinned(wl.n * 4), eng.pinned(wl.n * 2)
+    h_out = eng.pinned(wl.n * wl.rec)
+    eng.d2h(h_arena.ptr, b["arena"].ptr, nb)
+    eng.d2h(h_off.ptr, b["off64"].ptr, wl.n * 4)
+    eng.d2h(h_len.ptr, b["len"].ptr, wl.n * 2)
+    eng.sync()
+    d_arena, d_off, d_len = eng.alloc(nb), eng.alloc(wl.n * 4), eng.alloc(wl.n * 2)
+
+    def step():
+        eng.h2d(d_arena.ptr, h_arena.ptr, nb)
+        eng.h2d(d_off.ptr, h_off.ptr, wl.n * 4)
+        eng.h2d(d_len.ptr, h_len.ptr, wl.n * 2)
+        eng.rx_burst_dev(d_arena.ptr, d_off.ptr, d_len.ptr, wl.n, wl.out.ptr, wl.rec)
+        eng.d2h(h_out.ptr, wl.out.ptr, wl.n * wl.rec)
+
+    for _ in range(warmup):
+        step()
+    eng.sync()
+    barrier(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    barrier(device)
+    dt = max_over_ranks(time.perf_counter() - t0, device)
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    res = {"mpps": round(wl.n * steps * world / dt / 1e6, 2),
+           "gbs": round(wl.bytes_per_batch * steps * world / dt / 1e9, 2),
+           "h2d_bytes_per_step": nb + wl.n * 6, "d2h_bytes_per_step": wl.n * wl.rec,
+           "ms_per_step": round(dt / steps * 1e3, 3)}
+    for a in (h_arena, h_off, h_len, h_out):
+        a.free()
+    for a in (d_arena, d_off, d_len):
+        a.free()
+    return res
+
+
+def c5_leg(eng, n, steps, warmup, device, seed):
+    """Config 5: bidirectional, copy-inclusive, 2^20 flows.  tx: host-built IMIX frames ->
+    H2D -> checksum generate (ip_out, ip.c:97-118) -> D2H of the frames; rx: host frames ->
+    H2D -> parse+verify+classify -> D2H of the records.  One GPU's share (weak scaling)."""
+    flows = 1 << 20
+    tx = eng.synth(n=n, nflows=flows, mix=1, seed=seed + 5)
+    rx = eng.synth(n=n, nflows=flows, mix=1, seed=seed + 6)
+    eng.sync()
+    tcb, live = rxg.synthetic_tcb_table(flows)
+    eng.tcb_load(tcb, live)
+    eng.tcb_sync()
+    nb = tx["arena_bytes"]
+    lens = rx["len"].download(np.uint16, n)
+    tx_lens = tx["len"].download(np.uint16, n)
+    host = {k: eng.pinned(v) for k, v in (("tx", nb), ("rx", rx["arena_bytes"]), ("txo", n * 4),
+                                           ("txl", n * 2), ("rxo", n * 4), ("rxl", n * 2),
+                                           ("rec", n * 16))}
+    eng.d2h(host["tx"].ptr, tx["arena"].ptr, nb)
+    eng.d2h(host["rx"].ptr, rx["arena"].ptr, rx["arena_bytes"])
+    for k, d, sz in (("txo", tx["off64"], n * 4), ("txl", tx["len"], n * 2),
+                     ("rxo", rx["off64"], n * 4), ("rxl", rx["len"], n * 2)):
+        eng.d2h(host[k].ptr, d.ptr, sz)
+    eng.sync()
+    out = eng.alloc(n * 16)
+
+    def step():
+        eng.h2d(tx["arena"].ptr, host["tx"].ptr, nb)
+        eng.h2d(tx["off64"].ptr, host["txo"].ptr, n * 4)
+        eng.h2d(tx["len"].ptr, host["txl"].ptr, n * 2)
+        eng.tx_cksum_dev(tx["arena"].ptr, tx["off64"].ptr, tx["len"].ptr, n)
+        eng.d2h(host["tx"].ptr, tx["arena"].ptr, nb)
+        eng.h2d(rx["arena"].ptr, host["rx"].ptr, rx["arena_bytes"])
+        eng.h2d(rx["off64"].ptr, host["rxo"].ptr, n * 4)
+        eng.h2d(rx["len"].ptr, host["rxl"].ptr, n * 2)
+        eng.rx_burst_dev(rx["arena"].ptr, rx["off64"].ptr, rx["len"].ptr, n, out.ptr, 16)
+        eng.d2h(host["rec"].ptr, out.ptr, n * 16)
+
+    for _ in range(warmup):
+        step()
+    eng.sync()
+    eng.counters_reset()
+    barrier(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    barrier(device)
+    dt = max_over_ranks(time.perf_counter() - t0, device)
+    c = merge_counters(eng.counters(), device)
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rec = host["rec"].np[: n * 16].view(rxg.REC16_DTYPE)
+    ok = bool((rec["verdict"] == rxg.V_DISPATCH).all() and (rec["tcp_cksum"] == 0).all()
+              and int(c[0]) == n * steps * world and int(c[8]) == 0)
+    res = {"frames_per_dir_per_gpu": n, "flows": flows, "frame_mix": "imix 64/576/1500 7:4:1",
+           "mpps_per_direction": round(n * steps * world / dt / 1e6, 2),
+           "gbs_both_directions": round((int(lens.astype(np.uint64).sum()) + int(tx_lens.astype(np.uint64).sum()))
+                                        * steps * world / dt / 1e9, 2),
+           "ms_per_step": round(dt / steps * 1e3, 3), "counters_ok": ok}
+    for a in host.values():
+        a.free()
+    for d in list(tx.values()) + list(rx.values()) + [out]:
+        if isinstance(d, rxg.DevArray):
+            d.free()
+    return res
+
+
 def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
     """The oracle's faithful restatement of the reference rx path (port), on one host
     core, over a bounded sample of the same workload (first sample_n frames)."""
@@ -232,6 +341,9 @@ def main():
                                     and int(c2[7]) == 0 and int(c2[8]) == 0),
             }
             lw.free()
+        legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)
+        legs["c5_bidir_copy_inclusive"] = c5_leg(eng, args.frames, max(3, args.steps // 4), 1, device,
+                                                 seed)
         eng.tcb_load(tcb, live)
 
     cpu = None

@@ -156,17 +156,12 @@ __device__ __forceinline__ Fields unpark_fields(const uint32_t *sf, int lane)
     return F;
 }
 
-template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
-__device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uint32_t len, bool active,
-                                              int lane)
+template <int LPF, int NLOAD, bool NT>
+__device__ __forceinline__ void load_chunks(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                            int lane, uint32_t (&d)[NLOAD][4])
 {
-    constexpr bool TX = MODE == 0;
     const int gl = lane & (LPF - 1);
-    const int gbase = lane - gl;
-    const bool leader = active && gl == 0;
-    uint8_t *fp = const_cast<uint8_t *>(a.frames) + (size_t)off * 64u;
-
-    uint32_t d[NLOAD][4];
+    const uint8_t *fp = a.frames + (size_t)off * 64u;
 #pragma unroll
     for (int j = 0; j < NLOAD; ++j) {
         const int c = gl + j * LPF;
@@ -177,6 +172,31 @@ __device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uin
             d[j][0] = d[j][1] = d[j][2] = d[j][3] = 0u;
         }
     }
+}
+
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
+__device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                               int lane, uint32_t (&d)[NLOAD][4]);
+
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
+__device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                              int lane)
+{
+    uint32_t d[NLOAD][4];
+    load_chunks<LPF, NLOAD, NT>(a, off, len, active, lane, d);
+    return frame_fields<LPF, NLOAD, JUMBO, MODE, NT>(a, off, len, active, lane, d);
+}
+
+// Sums, header fields and (TX) checksum stores of the frames whose chunks are in d.
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
+__device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                               int lane, uint32_t (&d)[NLOAD][4])
+{
+    constexpr bool TX = MODE == 0;
+    const int gl = lane & (LPF - 1);
+    const int gbase = lane - gl;
+    const bool leader = active && gl == 0;
+    uint8_t *fp = const_cast<uint8_t *>(a.frames) + (size_t)off * 64u;
 
     // ---- header: dwords 1..11 (bytes 4..47) of the group's frame, gathered to every lane.
     uint32_t h1 = 0, h2 = 0;
@@ -249,9 +269,13 @@ __device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uin
     const uint32_t h6_ip = TX ? (h6 & 0xFFFF0000u) : h6;  // TX: hdr_checksum (bytes 24-25) = 0
     const uint32_t isum = hsum(h3 & 0xFFFF0000u) + hsum(h4) + hsum(h5) + hsum(h6_ip) + hsum(h7) +
                           hsum(h8 & 0xFFFFu);
-    const uint32_t thdr = hsum(h6 & 0xFFFF0000u) + hsum(h7) + hsum(h8 & region_mask(32, 26, E)) +
-                          hsum(h9 & region_mask(36, 26, E)) + hsum(h10 & region_mask(40, 26, E)) +
-                          hsum(h11 & region_mask(44, 26, E));
+    // region [26, E) with E >= 34: dwords at o >= 28 keep their low E - o bytes
+    uint32_t thdr = hsum(h6 & 0xFFFF0000u) + hsum(h7);
+    if (E >= 48)  // total_length >= 34: the whole TCP header is inside the span (common)
+        thdr += hsum(h8) + hsum(h9) + hsum(h10) + hsum(h11);
+    else
+        thdr += hsum(keep_low(h8, E - 32)) + hsum(keep_low(h9, E - 36)) + hsum(keep_low(h10, E - 40)) +
+                hsum(keep_low(h11, E - 44));
     // pseudo {.., 0x00, 0x06, htons(total_length - 20)} as little-endian words
     const uint32_t tall = tsum + thdr + 0x0600u + bswap16((tl - 20u) & 0xFFFFu);
     const uint32_t ip_ck = (~bswap16(fold16(isum))) & 0xFFFFu;
@@ -283,11 +307,12 @@ __device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uin
 
 // ---------------------------------------------------------- size-class dispatch ---
 //
-// Class c of a frame, by data_len:  <=64 | <=128 | <=256 | <=512 | <=1024 | <=1536 | <=2048 | more
+// Class of a frame by data_len: 0 <=64 | 1 <=128 | 2 <=256 | 3 <=512 | 8 <=768 | 4 <=1024 |
+// 5 <=1536 | 6 <=2048 | 7 more.  (<=768 runs 8 frames per round: IMIX's 576 B frames.)
 __device__ __forceinline__ int size_class(uint32_t len)
 {
     return len <= 64u ? 0 : len <= 128u ? 1 : len <= 256u ? 2 : len <= 512u ? 3
-         : len <= 1024u ? 4 : len <= 1536u ? 5 : len <= 2048u ? 6 : 7;
+         : len <= 768u ? 8 : len <= 1024u ? 4 : len <= 1536u ? 5 : len <= 2048u ? 6 : 7;
 }
 
 template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
@@ -336,7 +361,8 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
 
 // Phase B: lane i classifies frame i of the slice (all 64 probes in flight together) and
 // writes its record; the records of a slice are one contiguous 1 KiB / 3 KiB store.
-template <int MODE>
+// STRIP (experiment builds only): 1 = no frame loads, 2 = no TCB probe, 4 = no record store
+template <int MODE, int STRIP = 0>
 __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
                                                const Fields &F, WaveCounters &wc)
 {
@@ -355,7 +381,7 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     int32_t idx = -1;
     bool lhit = false, nslot = false;
     uint32_t st = RXG_STATE_NONE;
-    if (is_tcp) {
+    if (is_tcp && !(STRIP & 2)) {
         uint32_t hb = tuple_hash(ports, dst_raw, src_host) & a.t.bucket_mask;
         for (uint32_t probe = 0; probe <= a.t.bucket_mask; ++probe) {
             const uint4 *b = a.t.buckets + (size_t)hb * kSlotsPerBucket;
@@ -403,7 +429,7 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
                            (trunc ? RXG_F_TRUNC : 0u);
     const int32_t datalen = (int32_t)tl - (int32_t)(vihl & 0xFu) * 4 - (int32_t)(doff >> 4) * 4;
 
-    if (valid) {
+    if (valid && !(STRIP & 4)) {
         uint4 q0;
         q0.x = (uint32_t)idx;
         q0.y = ipc | (tcc << 16);
@@ -445,11 +471,57 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     wcount(wc, RXG_C_DISPATCH, is_tcp && verdict == RXG_V_DISPATCH);
 }
 
-template <int MODE, int CMASK, bool NT>
+// An all-small slice (64 frames of <= 64 bytes): lane l loads chunk l&3 of frame 16j + l/4
+// (instruction j covers 16 whole frames, 1 KiB, coalesced), writes it to the wave's LDS
+// at [frame][chunk], and after a wave barrier lane i reads back frame i's 64 bytes.
+template <bool NT>
+__device__ __forceinline__ void load_small_slice(const RxArgs &a, uint32_t off, uint32_t len, int lane,
+                                                 uint32_t *sf, uint32_t (&d)[4][4])
+{
+    uint4 v[4];
+    const int ch = lane & 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int fr = 16 * j + (lane >> 2);
+        const uint32_t foff = lane_read(off, fr), flen = lane_read(len, fr);
+        if ((uint32_t)(ch * 16) < flen)
+            v[j] = load16<NT>(a.frames + (size_t)foff * 64u + ch * 16);
+        else
+            v[j] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    uint4 *t = reinterpret_cast<uint4 *>(sf);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[j * 64 + lane] = v[j];  // [frame 16j + l/4][chunk l&3]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint4 q = t[lane * 4 + c];
+        d[c][0] = q.x; d[c][1] = q.y; d[c][2] = q.z; d[c][3] = q.w;
+    }
+    __builtin_amdgcn_wave_barrier();  // reads done before the LDS is reused
+}
+
+__device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane, uint32_t &off, uint32_t &len)
+{
+    const uint32_t f = s * 64u + (uint32_t)lane;
+    off = 0u;
+    len = 0u;
+    if (s < ((a.n + 63u) >> 6) && f < a.n) {
+        off = a.off64[f];
+        len = a.len[f];
+    }
+}
+
+template <int MODE, int CMASK, bool NT, bool PIPE = false, int STRIP = 0, bool SMALL_COALESCED = true>
 __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 {
     constexpr int NF = MODE == 48 ? NF48 : NF16;
-    __shared__ uint32_t s_fields[4][MODE == 0 ? 1 : NF * 64];
+    // per-wave LDS: the parked fields of the general path, or the 4 KiB transpose of an
+    // all-small slice (never both at once)
+    constexpr int kWaveLds = MODE == 0 ? 1 : (NF * 64 > 1024 ? NF * 64 : 1024);
+    __shared__ __attribute__((aligned(16))) uint32_t s_fields[4][kWaveLds];
     __shared__ unsigned long long s_cnt[4][RXG_NCOUNTERS];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
@@ -463,37 +535,63 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     for (int k = 0; k < RXG_NCOUNTERS; ++k) wc.c[k] = 0u;
     unsigned long long bytes = 0ull;
 
-    // descriptors of the first slice; each iteration prefetches the next slice's
+    // Descriptors: (c_off, c_len) for slice s, (n_off, n_len) for slice s + nwaves, whose
+    // loads are always in flight while slice s is processed.
     uint32_t s = wave;
-    uint32_t noff = 0, nlen = 0;
-    {
-        const uint32_t f = s * 64u + (uint32_t)lane;
-        if (s < nslices && f < a.n) { noff = a.off64[f]; nlen = a.len[f]; }
-    }
-    for (; s < nslices; s += nwaves) {
+    uint32_t c_off = 0, c_len = 0, n_off = 0, n_len = 0;
+    load_desc(a, s, lane, c_off, c_len);
+    load_desc(a, s + nwaves, lane, n_off, n_len);
+    while (s < nslices) {
         const uint32_t f = s * 64u + (uint32_t)lane;
         const bool valid = f < a.n;
-        const uint32_t off = noff, len = valid ? nlen : 0u;
-        {
-            const uint32_t f2 = (s + nwaves) * 64u + (uint32_t)lane;
-            noff = 0; nlen = 0;
-            if (s + nwaves < nslices && f2 < a.n) { noff = a.off64[f2]; nlen = a.len[f2]; }
-        }
-        const int cls = valid ? size_class(len) : 8;
-        bytes += len;
+        const uint32_t off = c_off, len = valid ? c_len : 0u;
+        const int cls = valid ? size_class(len) : 9;
         if constexpr (MODE != 0 && (CMASK & 1)) {
             if (__ballot(cls == 0) == ~0ull) {
-                // every frame of the slice is <= 64 bytes: lane i owns frame i end to end,
-                // fields stay in registers (no LDS round trip)
-                const Fields F = frame_round<1, 4, false, MODE, false>(a, off, len, true, lane);
-                classify_store<MODE>(a, f, true, len, F, wc);
+                // All-small pipeline: every frame of the slice is <= 64 bytes, lane i owns
+                // frame i end to end (fields stay in registers), and the NEXT all-small
+                // slice's frame loads are issued before this slice is classified.
+                uint32_t d[4][4], e[4][4];
+                uint32_t cur_len = len;
+                if constexpr (STRIP & 1) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) d[j][w] = (uint32_t)lane * 0x01000193u + j + w;
+                } else if constexpr (SMALL_COALESCED) {
+                    load_small_slice<false>(a, off, cur_len, lane, sf, d);
+                } else {
+                    load_chunks<1, 4, false>(a, off, cur_len, true, lane, d);
+                }
+                for (;;) {
+                    const uint32_t s2 = s + nwaves;
+                    const uint32_t f2 = s2 * 64u + (uint32_t)lane;
+                    const bool small2 = PIPE && __ballot(s2 < nslices && f2 < a.n && n_len <= 64u) == ~0ull;
+                    if (small2) load_chunks<1, 4, false>(a, n_off, n_len, true, lane, e);
+                    uint32_t nn_off = 0, nn_len = 0;
+                    load_desc(a, s2 + nwaves, lane, nn_off, nn_len);
+                    const Fields F = frame_fields<1, 4, false, MODE, false>(a, c_off, cur_len, true, lane, d);
+                    classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, cur_len, F, wc);
+                    bytes += cur_len;
+                    s = s2;
+                    c_off = n_off; c_len = n_len;
+                    n_off = nn_off; n_len = nn_len;
+                    if (!small2) break;
+                    cur_len = c_len;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) d[j][w] = e[j][w];
+                }
                 continue;
             }
         }
+        bytes += len;
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT>(a, cls, off, len, lane, sf);
@@ -508,6 +606,9 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
             classify_store<MODE>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
         }
+        s += nwaves;
+        c_off = n_off; c_len = n_len;
+        load_desc(a, s + nwaves, lane, n_off, n_len);
     }
 
     if (a.counters == nullptr) return;
@@ -667,6 +768,15 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 1: hipLaunchKernelGGL((rx_kernel<16, 0x01, false>), dim3(blocks), dim3(256), 0, st, a); break;
         case 2: hipLaunchKernelGGL((rx_kernel<16, 0x20, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 3: hipLaunchKernelGGL((rx_kernel<16, 0xFF, false>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, true>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 5: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 6: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 1>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 7: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 2>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 4>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 9: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 6>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 10: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 7>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 11: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, false>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 12: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 0, false>), dim3(blocks), dim3(256), 0, st, a); break;
         default: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
     } else if (L.mode == 48) {

@@ -257,6 +257,24 @@ class DevArray:
             self.ptr = None
 
 
+class PinnedArray:
+    """Page-locked host memory (hipHostMalloc) viewed as a numpy uint8 array."""
+
+    def __init__(self, eng: "Engine", nbytes: int):
+        self.eng, self.nbytes = eng, int(nbytes)
+        p = C.c_void_p()
+        _check(_lib.rxg_host_alloc_pinned(eng.ctx, max(self.nbytes, 1), C.byref(p)),
+               "rxg_host_alloc_pinned")
+        self.ptr = p.value
+        self.np = np.ctypeslib.as_array((C.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            self.np = None
+            _lib.rxg_host_free_pinned(self.eng.ctx, self.ptr)
+            self.ptr = None
+
+
 class Engine:
     """One rxg context on one GPU (include/rxg.h: rxg_init .. rxg_fini)."""
 
@@ -288,6 +306,15 @@ class Engine:
 
     def alloc(self, nbytes: int) -> DevArray:
         return DevArray(self, nbytes)
+
+    def pinned(self, nbytes: int) -> PinnedArray:
+        return PinnedArray(self, nbytes)
+
+    def h2d(self, dst: int, src: int, nbytes: int, stream=None):
+        _check(_lib.rxg_memcpy_h2d(self.ctx, dst, src, nbytes, stream), "rxg_memcpy_h2d")
+
+    def d2h(self, dst: int, src: int, nbytes: int, stream=None):
+        _check(_lib.rxg_memcpy_d2h(self.ctx, dst, src, nbytes, stream), "rxg_memcpy_d2h")
 
     def to_device(self, a: np.ndarray) -> DevArray:
         d = DevArray(self, a.nbytes)
