@@ -29,6 +29,7 @@ constexpr int kSlotsPerBucket = 4;
 constexpr uint32_t kIdxMask = 0x00FFFFFFu;
 constexpr int kStateShift = 24;
 constexpr int32_t kMaxTcbs = 0x00FFFFFF;  // indices 0 .. kMaxTcbs-1
+constexpr int kKernelCounterRows = RXG_COUNTER_ROWS - 1;  // the last row is the host's
 
 RXG_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
@@ -82,13 +83,17 @@ RXG_HD uint32_t imix_len(int pos)
     return ((pat >> pos) & 1u) ? 576u : 64u;
 }
 
+// ARP mirror: open-addressing set of host-order IPv4 addresses, slot = {ip, used}.
+RXG_HD uint32_t arp_hash(uint32_t ip) { return tuple_hash(ip, 0x41525000u, 0u); }
+
 struct DevTable {
     const uint4 *buckets;  // nbuckets * 4 slots
     const int32_t *listen; // 65536
+    const uint2 *arp;      // ARP mirror slots, or nullptr (mirror disabled)
     uint32_t bucket_mask;  // nbuckets - 1
     int32_t ntcb;
     int32_t min_null;      // INT32_MAX if none
-    int32_t pad;
+    uint32_t arp_mask;     // ARP slots - 1
 };
 
 }  // namespace rxg

@@ -75,6 +75,27 @@ struct rxg_ctx {
 
     unsigned long long *counters = nullptr;
 
+    // mirror changes since the last clear, for rxg_rx_replay's re-classification
+    uint64_t gen = 0, burst_gen = 0;
+    std::vector<int32_t> touched;  // dports (old and new) of changed slots
+    bool touched_all = false;      // whole table replaced
+    bool touched_pass2 = false;    // a slot was removed / NULL slots appeared (pass-2 flag)
+
+    // the last burst's device batch (re-classification reads it again)
+    const uint8_t *last_frames = nullptr;
+    const uint32_t *last_off = nullptr;
+    const uint16_t *last_len = nullptr;
+    uint32_t last_n = 0;
+    DevBuf d_sel, d_fix;
+
+    // ARP mirror (host set + device open-addressing table)
+    bool arp_enabled = false, arp_dirty = false;
+    std::vector<uint32_t> arp_ips;              // in add_mac order
+    std::unordered_map<uint32_t, int> arp_set;
+    std::unordered_map<uint32_t, int> arp_since_burst;  // learned after the last burst
+    DevBuf d_arp;
+    uint32_t arp_mask = 0;
+
     // host-buffer burst staging
     uint32_t max_batch = 0;
     uint64_t max_bytes = 0;
@@ -177,7 +198,7 @@ extern "C" int rxg_fini(rxg_ctx *c)
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->buckets, &c->listen})
+    for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp})
         if (b->p) (void)hipFree(b->p);
     if (c->counters) (void)hipFree(c->counters);
     if (c->h_arena) (void)hipHostFree(c->h_arena);
@@ -218,11 +239,16 @@ extern "C" int rxg_tcb_upsert(rxg_ctx *c, int32_t idx, const rxg_tcb_tuple *t)
 {
     if (!c || !t) return fail(-EINVAL, "rxg_tcb_upsert: NULL argument");
     if (t->state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_upsert: state %u", t->state);
+    const size_t old_n = c->tcb.size();
     int rc = grow_to(c, idx);
     if (rc) return rc;
+    if ((size_t)idx > old_n) c->touched_pass2 = true;  // slots old_n..idx-1 appear as NULL
+    if ((size_t)idx < old_n && c->live[idx]) c->touched.push_back(c->tcb[idx].dport);
+    c->touched.push_back(t->dport);
     c->tcb[idx] = *t;
     c->live[idx] = 1;
     c->dirty = true;
+    c->gen++;
     return 0;
 }
 
@@ -231,8 +257,11 @@ extern "C" int rxg_tcb_remove(rxg_ctx *c, int32_t idx)
     if (!c) return fail(-EINVAL, "rxg_tcb_remove: ctx NULL");
     if (idx < 0 || (size_t)idx >= c->tcb.size())
         return fail(-EINVAL, "rxg_tcb_remove: index %d outside Ntcb %zu", idx, c->tcb.size());
+    if (c->live[idx]) c->touched.push_back(c->tcb[idx].dport);
+    c->touched_pass2 = true;
     c->live[idx] = 0;
     c->dirty = true;
+    c->gen++;
     return 0;
 }
 
@@ -242,8 +271,10 @@ extern "C" int rxg_tcb_set_state(rxg_ctx *c, int32_t idx, uint8_t state)
     if (state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_set_state: state %u", state);
     if (idx < 0 || (size_t)idx >= c->tcb.size() || !c->live[idx])
         return fail(-EINVAL, "rxg_tcb_set_state: index %d is not a live slot", idx);
+    c->touched.push_back(c->tcb[idx].dport);
     c->tcb[idx].state = state;
     c->dirty = true;
+    c->gen++;
     return 0;
 }
 
@@ -260,6 +291,8 @@ extern "C" int rxg_tcb_load(rxg_ctx *c, const rxg_tcb_tuple *tcbs, const uint8_t
     else
         c->live.assign((size_t)ntcb, 1);
     c->dirty = true;
+    c->touched_all = true;
+    c->gen++;
     return 0;
 }
 
@@ -337,6 +370,64 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
     return 0;
 }
 
+// ----------------------------------------------------------------------- ARP mirror ---
+extern "C" int rxg_arp_learned(rxg_ctx *c, uint32_t ip)
+{
+    if (!c) return fail(-EINVAL, "rxg_arp_learned: ctx NULL");
+    c->arp_enabled = true;
+    if (c->arp_set.emplace(ip, 1).second) {
+        c->arp_ips.push_back(ip);
+        c->arp_dirty = true;
+    }
+    c->arp_since_burst.emplace(ip, 1);
+    return 0;
+}
+
+extern "C" int rxg_arp_load(rxg_ctx *c, const uint32_t *ips, uint32_t n)
+{
+    if (!c || (n && !ips)) return fail(-EINVAL, "rxg_arp_load: bad arguments");
+    c->arp_enabled = true;
+    c->arp_ips.clear();
+    c->arp_set.clear();
+    for (uint32_t i = 0; i < n; ++i)
+        if (c->arp_set.emplace(ips[i], 1).second) c->arp_ips.push_back(ips[i]);
+    c->arp_dirty = true;
+    return 0;
+}
+
+extern "C" int32_t rxg_arp_count(rxg_ctx *c) { return c ? (int32_t)c->arp_ips.size() : -EINVAL; }
+
+extern "C" int rxg_arp_disable(rxg_ctx *c)
+{
+    if (!c) return fail(-EINVAL, "rxg_arp_disable: ctx NULL");
+    c->arp_enabled = false;
+    c->arp_ips.clear();
+    c->arp_set.clear();
+    c->arp_since_burst.clear();
+    return 0;
+}
+
+static int arp_sync(rxg_ctx *c)
+{
+    if (!c->arp_enabled || !c->arp_dirty) return 0;
+    uint32_t ns = 16;
+    while ((uint64_t)ns < (uint64_t)c->arp_ips.size() * 2u) ns <<= 1;
+    std::vector<uint32_t> slots((size_t)ns * 2u, 0u);
+    for (uint32_t ip : c->arp_ips) {
+        uint32_t h = arp_hash(ip) & (ns - 1);
+        while (slots[(size_t)h * 2 + 1]) h = (h + 1) & (ns - 1);
+        slots[(size_t)h * 2] = ip;
+        slots[(size_t)h * 2 + 1] = 1;
+    }
+    int rc = ensure(c->d_arp, slots.size() * 4);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(c->d_arp.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    c->arp_mask = ns - 1;
+    c->arp_dirty = false;
+    return 0;
+}
+
 static DevTable table_view(const rxg_ctx *c)
 {
     DevTable t;
@@ -345,7 +436,8 @@ static DevTable table_view(const rxg_ctx *c)
     t.bucket_mask = c->bucket_mask;
     t.ntcb = c->dev_ntcb;
     t.min_null = c->dev_min_null;
-    t.pad = 0;
+    t.arp = c->arp_enabled ? (const uint2 *)c->d_arp.p : nullptr;
+    t.arp_mask = c->arp_mask;
     return t;
 }
 
@@ -360,7 +452,18 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
     int rc = set_device(c);
     if (rc) return rc;
     if (c->dirty && (rc = rxg_tcb_sync(c))) return rc;
+    if ((rc = arp_sync(c))) return rc;
+    c->arp_since_burst.clear();
+    c->last_frames = (const uint8_t *)b->frames;
+    c->last_off = b->off64;
+    c->last_len = b->len;
+    c->last_n = b->n;
+    // the records reflect the mirror as of now: changes are tracked from here (replay)
+    c->touched.clear();
+    c->touched_all = c->touched_pass2 = false;
+    c->burst_gen = c->gen;
     LaunchRx L;
+    std::memset(&L, 0, sizeof L);
     L.frames = (const uint8_t *)b->frames;
     L.off64 = b->off64;
     L.len = b->len;
@@ -451,7 +554,8 @@ extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
     if (!c || !out) return fail(-EINVAL, "rxg_counters_read: NULL argument");
     HIP_OK(hipStreamSynchronize(c->stream));
     std::vector<uint64_t> rows((size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS);
-    HIP_OK(hipMemcpy(rows.data(), c->counters, kCounterBytes, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpyAsync(rows.data(), c->counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
     for (int k = 0; k < RXG_NCOUNTERS; ++k) {
         uint64_t v = 0;
         for (int r = 0; r < RXG_COUNTER_ROWS; ++r) v += rows[(size_t)r * RXG_NCOUNTERS + k];
@@ -463,6 +567,51 @@ extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
 extern "C" void *rxg_counters_dev(rxg_ctx *c) { return c ? (void *)c->counters : nullptr; }
 
 // ------------------------------------------------------------------------- replay ---
+static inline bool rec_is_tcp(const rxg_rec16 &r)
+{
+    return r.verdict == RXG_V_DISPATCH || r.verdict == RXG_V_RST_NOPCB || r.verdict == RXG_V_RST_LISTEN_NONSYN;
+}
+
+// Counter contributions of one TCP record (the kernel's definition; only the fields a
+// re-classification can change).
+static void tcp_record_counters(const rxg_rec16 &r, int64_t sign, int64_t *d)
+{
+    if (r.flags & RXG_F_REF_NULLSLOT) d[RXG_C_REF_NULLSLOT] += sign;
+    if (r.tcb_idx >= 0) d[(r.flags & RXG_F_LISTEN) ? RXG_C_TCB_HIT_LISTEN : RXG_C_TCB_HIT_EXACT] += sign;
+    if (r.verdict == RXG_V_RST_NOPCB) d[RXG_C_NOPCB] += sign;
+    if (r.verdict == RXG_V_RST_LISTEN_NONSYN) d[RXG_C_LISTEN_NONSYN] += sign;
+    if (r.verdict == RXG_V_DISPATCH) d[RXG_C_DISPATCH] += sign;
+}
+
+// Re-classify frames sel[0..k) of the last burst against the current mirror (GPU).
+static int reclassify(rxg_ctx *c, const std::vector<uint32_t> &sel, std::vector<rxg_rec16> &out)
+{
+    int rc;
+    if (!c->last_frames || !c->last_off || !c->last_len)
+        return fail(-EINVAL, "rxg_rx_replay: no burst on this context to re-classify against");
+    if ((rc = ensure(c->d_sel, sel.size() * 4))) return rc;
+    if ((rc = ensure(c->d_fix, sel.size() * sizeof(rxg_rec16)))) return rc;
+    if (c->dirty && (rc = rxg_tcb_sync(c))) return rc;
+    HIP_OK(hipMemcpyAsync(c->d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, c->stream));
+    LaunchRx L;
+    std::memset(&L, 0, sizeof L);
+    L.frames = c->last_frames;
+    L.off64 = c->last_off;
+    L.len = c->last_len;
+    L.sel = (const uint32_t *)c->d_sel.p;
+    L.n = (uint32_t)sel.size();
+    L.mode = RXG_REC16;
+    L.out = (uint8_t *)c->d_fix.p;
+    L.table = table_view(c);
+    L.counters = nullptr;  // corrections go to the host row instead
+    L.max_blocks = c->grid_rec16 ? c->grid_rec16 : 1024;
+    HIP_OK(launch_rx(L, c->stream));
+    out.resize(sel.size());
+    HIP_OK(hipMemcpyAsync(out.data(), c->d_fix.p, sel.size() * sizeof(rxg_rec16), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 // The side effects of etherin.c:21-35, ip.c:26-39 and tcp_in.c:47-72, in packet order.
 extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const *mbufs,
                              void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t stride)
@@ -470,12 +619,57 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
     if (!c || !ops || (n && (!mbufs || !frames || !recs)))
         return fail(-EINVAL, "rxg_rx_replay: NULL argument");
     if (stride != RXG_REC16 && stride != RXG_REC48) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
+    if (n && c->last_n != n) return fail(-EINVAL, "rxg_rx_replay: n=%u but the last burst had %u frames", n, c->last_n);
+    std::vector<rxg_rec16> cur(n);
+    for (uint32_t i = 0; i < n; ++i) cur[i] = *(const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
+    std::vector<uint8_t> stale(n, 0);
+    int64_t delta[RXG_NCOUNTERS] = {0};
+    std::vector<uint8_t> hit(65536, 0);
+    // Mark the TCP packets j >= j0 whose classification the tracked changes can affect,
+    // then forget the changes.  The dport is re-read from the frame (>= 54 bytes unless
+    // RXG_F_TRUNC, which is marked conservatively).
+    auto mark_from = [&](uint32_t j0) {
+        for (int32_t d : c->touched)
+            if (d >= 0 && d <= 0xFFFF) hit[d] = 1;
+        for (uint32_t j = j0; j < n; ++j) {
+            const rxg_rec16 &q = cur[j];
+            if (!rec_is_tcp(q) || stale[j]) continue;
+            bool st = c->touched_all || (q.flags & RXG_F_TRUNC);
+            if (!st) {
+                const uint8_t *g = (const uint8_t *)frames[j];
+                st = hit[((uint32_t)g[36] << 8) | g[37]] != 0;
+            }
+            if (!st && c->touched_pass2) st = q.tcb_idx < 0 || (q.flags & RXG_F_LISTEN);
+            if (st) stale[j] = 1;
+        }
+        for (int32_t d : c->touched)
+            if (d >= 0 && d <= 0xFFFF) hit[d] = 0;
+        c->touched.clear();
+        c->touched_all = c->touched_pass2 = false;
+    };
+    if (c->gen != c->burst_gen) mark_from(0);  // changes made between the burst and now
+
     for (uint32_t i = 0; i < n; ++i) {
-        const rxg_rec16 *r = (const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
+        if (stale[i]) {  // re-classify every stale packet from here on in one launch
+            std::vector<uint32_t> sel;
+            for (uint32_t j = i; j < n; ++j)
+                if (stale[j]) sel.push_back(j);
+            std::vector<rxg_rec16> fix;
+            int rc = reclassify(c, sel, fix);
+            if (rc) return rc;
+            for (size_t k = 0; k < sel.size(); ++k) {
+                tcp_record_counters(cur[sel[k]], -1, delta);
+                tcp_record_counters(fix[k], +1, delta);
+                cur[sel[k]] = fix[k];
+                stale[sel[k]] = 0;
+            }
+        }
+        const rxg_rec16 &r = cur[i];
         void *m = mbufs[i];
         uint8_t *f = (uint8_t *)frames[i];
         void *ip = f + RXG_OFF_IP, *tcp = f + RXG_OFF_TCP;
-        switch (r->verdict) {
+        const uint64_t gen_before = c->gen;
+        switch (r.verdict) {
         case RXG_V_ARP:
             if (ops->arp_in) ops->arp_in(ops->user, m);
             if (ops->free_mbuf) ops->free_mbuf(ops->user, m);
@@ -487,20 +681,41 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         default: {
             // ip.c:30-32 ARP learn on the host-order source address
             const uint32_t src = ((uint32_t)f[26] << 24) | ((uint32_t)f[27] << 16) | ((uint32_t)f[28] << 8) | f[29];
-            unsigned char mac[6];
-            if (ops->get_mac && ops->add_mac && ops->get_mac(ops->user, src, mac) == 0)
-                ops->add_mac(ops->user, src, f + 6);
-            if (r->verdict == RXG_V_RST_NOPCB || r->verdict == RXG_V_RST_LISTEN_NONSYN) {
+            if (c->arp_enabled) {
+                // the mirror answers get_mac: unknown at the burst and not added since
+                if ((r.flags & RXG_F_ARP_LEARN) && ops->add_mac && !c->arp_since_burst.count(src)) {
+                    ops->add_mac(ops->user, src, f + 6);
+                    rxg_arp_learned(c, src);  // idempotent if the caller's add_mac mirrors too
+                }
+            } else {
+                unsigned char mac[6];
+                if (ops->get_mac && ops->add_mac && ops->get_mac(ops->user, src, mac) == 0)
+                    ops->add_mac(ops->user, src, f + 6);
+            }
+            if (r.verdict == RXG_V_RST_NOPCB || r.verdict == RXG_V_RST_LISTEN_NONSYN) {
                 if (ops->free_mbuf) ops->free_mbuf(ops->user, m);
                 if (ops->send_reset) ops->send_reset(ops->user, ip, tcp);
             } else {  // RXG_V_DISPATCH
                 const uint32_t seq = ((uint32_t)f[38] << 24) | ((uint32_t)f[39] << 16) | ((uint32_t)f[40] << 8) | f[41];
                 const uint32_t ack = ((uint32_t)f[42] << 24) | ((uint32_t)f[43] << 16) | ((uint32_t)f[44] << 8) | f[45];
-                if (ops->on_segment) ops->on_segment(ops->user, r->tcb_idx, seq, ack);
-                if (ops->tcpswitch) ops->tcpswitch(ops->user, r->tcb_idx, r->state, tcp, ip, m);
+                if (ops->on_segment) ops->on_segment(ops->user, r.tcb_idx, seq, ack);
+                if (ops->tcpswitch) ops->tcpswitch(ops->user, r.tcb_idx, r.state, tcp, ip, m);
             }
         }
         }
+        if (c->gen != gen_before) mark_from(i + 1);  // the handlers changed the table
+    }
+    c->burst_gen = c->gen;
+    bool nz = false;
+    for (int k = 0; k < RXG_NCOUNTERS; ++k) nz |= delta[k] != 0;
+    if (nz) {  // add the corrections to the host row of the counter block
+        uint64_t row[RXG_NCOUNTERS];
+        unsigned long long *dst = c->counters + (size_t)(RXG_COUNTER_ROWS - 1) * RXG_NCOUNTERS;
+        HIP_OK(hipMemcpyAsync(row, dst, sizeof row, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        for (int k = 0; k < RXG_NCOUNTERS; ++k) row[k] += (uint64_t)delta[k];
+        HIP_OK(hipMemcpyAsync(dst, row, sizeof row, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
     }
     return 0;
 }

@@ -10,6 +10,7 @@ struct LaunchRx {
     const uint8_t *frames;
     const uint32_t *off64;
     const uint16_t *len;
+    const uint32_t *sel;   // optional selection list (re-classification), else nullptr
     uint32_t n;
     int mode;              // 16 / 48: receive records of that size; 0: tx checksum generate
     uint8_t *out;

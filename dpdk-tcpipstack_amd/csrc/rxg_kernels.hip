@@ -91,6 +91,7 @@ struct RxArgs {
     const uint8_t *frames;
     const uint32_t *off64;
     const uint16_t *len;
+    const uint32_t *sel;  // optional: logical frame i is physical frame sel[i] (re-classify)
     uint32_t n;
     uint32_t pad;
     uint8_t *out;
@@ -375,6 +376,19 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     const bool is_tcp = is_ip && proto == RXG_IPPROTO_TCP;
     const bool is_arp = valid && et == RXG_ETHER_TYPE_ARP;
     const bool trunc = valid && len < 54u;
+    // ip.c:30-32: would get_mac(ntohl(src)) fail?  (ARP mirror enabled only)
+    bool arp_learn = false;
+    if (is_tcp && a.t.arp != nullptr) {
+        const uint32_t ip = bswap32(src_raw);
+        uint32_t h = arp_hash(ip) & a.t.arp_mask;
+        arp_learn = true;
+        for (uint32_t probe = 0; probe <= a.t.arp_mask; ++probe) {
+            const uint2 e = a.t.arp[h];
+            if (!e.y) break;
+            if (e.x == ip) { arp_learn = false; break; }
+            h = (h + 1u) & a.t.arp_mask;
+        }
+    }
     const uint32_t src_host = bswap32(src_raw);
 
     // ---- findtcb (tcp_tcb.c:127-173): pass 1 = exact-tuple bucket probe, pass 2 = listener
@@ -426,7 +440,7 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     const uint32_t flags = ((is_ip && ipc == 0u) ? RXG_F_IP_OK : 0u) |
                            ((is_tcp && tcc == 0u) ? RXG_F_TCP_OK : 0u) |
                            (lhit ? RXG_F_LISTEN : 0u) | (nslot ? RXG_F_REF_NULLSLOT : 0u) |
-                           (trunc ? RXG_F_TRUNC : 0u);
+                           (trunc ? RXG_F_TRUNC : 0u) | (arp_learn ? RXG_F_ARP_LEARN : 0u);
     const int32_t datalen = (int32_t)tl - (int32_t)(vihl & 0xFu) * 4 - (int32_t)(doff >> 4) * 4;
 
     if (valid && !(STRIP & 4)) {
@@ -509,8 +523,9 @@ __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane,
     off = 0u;
     len = 0u;
     if (s < ((a.n + 63u) >> 6) && f < a.n) {
-        off = a.off64[f];
-        len = a.len[f];
+        const uint32_t pf = a.sel ? a.sel[f] : f;
+        off = a.off64[pf];
+        len = a.len[pf];
     }
 }
 
@@ -628,7 +643,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         const int k = threadIdx.x;
         const unsigned long long v = s_cnt[0][k] + s_cnt[1][k] + s_cnt[2][k] + s_cnt[3][k];
         // replica row per workgroup (rxg.h RXG_COUNTER_ROWS): 32 adders per line, not 2048
-        if (v) atomicAdd(&a.counters[(blockIdx.x % RXG_COUNTER_ROWS) * RXG_NCOUNTERS + k], v);
+        if (v) atomicAdd(&a.counters[(blockIdx.x % kKernelCounterRows) * RXG_NCOUNTERS + k], v);
     }
 }
 
@@ -751,6 +766,7 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     a.frames = L.frames;
     a.off64 = L.off64;
     a.len = L.len;
+    a.sel = L.sel;
     a.n = L.n;
     a.pad = 0;
     a.out = L.out;

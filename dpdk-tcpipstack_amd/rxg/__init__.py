@@ -140,6 +140,10 @@ def load_library(path: str = LIB_PATH):
         "rxg_tcb_load": (C.c_int, [vp, vp, vp, i32]),
         "rxg_tcb_sync": (C.c_int, [vp]),
         "rxg_tcb_count": (i32, [vp]),
+        "rxg_arp_load": (C.c_int, [vp, vp, u32]),
+        "rxg_arp_learned": (C.c_int, [vp, u32]),
+        "rxg_arp_count": (i32, [vp]),
+        "rxg_arp_disable": (C.c_int, [vp]),
         "rxg_rx_burst_dev": (C.c_int, [vp, C.POINTER(DevBatch), vp]),
         "rxg_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
         "rxg_tx_cksum_dev": (C.c_int, [vp, C.POINTER(DevTxBatch), vp]),
@@ -344,6 +348,20 @@ class Engine:
 
     def tcb_count(self) -> int:
         return _lib.rxg_tcb_count(self.ctx)
+
+    # --- ARP mirror (ip.c:30-32 learn, arp.c add_mac)
+    def arp_load(self, ips):
+        a = np.ascontiguousarray(np.asarray(ips, dtype=np.uint32))
+        _check(_lib.rxg_arp_load(self.ctx, _ptr(a) if len(a) else None, len(a)), "rxg_arp_load")
+
+    def arp_learned(self, ip: int):
+        _check(_lib.rxg_arp_learned(self.ctx, ip & 0xFFFFFFFF), "rxg_arp_learned")
+
+    def arp_count(self) -> int:
+        return _lib.rxg_arp_count(self.ctx)
+
+    def arp_disable(self):
+        _check(_lib.rxg_arp_disable(self.ctx), "rxg_arp_disable")
 
     # --- bursts
     def rx_burst_dev(self, frames: int, off64: int, lens: int, n: int, out: int,

@@ -94,7 +94,10 @@ enum rxg_rec_flag {
                                   rxg skips the slot and reports it                        */
     RXG_F_TRUNC = 0x10,        /* frame shorter than the 54 bytes the path reads; bytes at
                                   and beyond data_len are read as zero                      */
-    RXG_F_ARP_LEARN = 0x20     /* reserved: first sighting of src IP (ip.c:30-32)            */
+    RXG_F_ARP_LEARN = 0x20     /* TCP packet whose host-order source IP is not in the ARP
+                                  mirror as of the burst: ip.c:30-32 would call add_mac
+                                  unless an earlier packet of the burst already added it
+                                  (only computed while the ARP mirror is enabled)           */
 };
 
 /*
@@ -210,6 +213,17 @@ int rxg_tcb_sync(rxg_ctx *ctx);
 /* Current Ntcb of the mirror. */
 int32_t rxg_tcb_count(rxg_ctx *ctx);
 
+/* ARP mirror (optional).  The reference keeps an IP -> MAC list that ip_in walks twice per
+   packet (print_arp_table + get_mac, ip.c:26-32, arp.c:215-280).  Once a caller mirrors
+   every add_mac (arp.c:282-317) with rxg_arp_learned, bursts flag each TCP packet whose
+   source is unknown (RXG_F_ARP_LEARN) and rxg_rx_replay calls add_mac for the first such
+   packet per address without walking the list: same final list, same order. */
+int rxg_arp_load(rxg_ctx *ctx, const uint32_t *ipv4_host, uint32_t n);
+int rxg_arp_learned(rxg_ctx *ctx, uint32_t ipv4_host);
+int32_t rxg_arp_count(rxg_ctx *ctx);
+/* Stop mirroring (RXG_F_ARP_LEARN is no longer computed; replay walks get_mac again). */
+int rxg_arp_disable(rxg_ctx *ctx);
+
 /* ------------------------------------------------------------------------- */
 /* Receive burst: parse + checksum + classify.  Pure: no frees, no side       */
 /* effects, counters only.                                                    */
@@ -267,9 +281,10 @@ int rxg_tx_cksum_dev(rxg_ctx *ctx, const rxg_dev_tx_batch *b, void *stream);
 int rxg_counters_reset(rxg_ctx *ctx, void *stream);
 /* Synchronous read of the RXG_NCOUNTERS uint64 counters (the replica rows summed). */
 int rxg_counters_read(rxg_ctx *ctx, uint64_t *out);
-/* The device keeps RXG_COUNTER_ROWS replicas of the counter block so that workgroups do
-   not all add to one cache line; counter k = sum over rows r of block[r][k]. */
-#define RXG_COUNTER_ROWS 64
+/* The device keeps RXG_COUNTER_ROWS rows of the counter block: 64 replicas the kernels add
+   into (so that workgroups do not all add to one cache line) and one row of corrections
+   written by rxg_rx_replay when it re-classifies packets; counter k = sum over rows. */
+#define RXG_COUNTER_ROWS 65
 /* Device address of the uint64[RXG_COUNTER_ROWS][RXG_NCOUNTERS] block: an in-place RCCL
    all-reduce (sum) over it followed by rxg_counters_read merges counters across GPUs. */
 void *rxg_counters_dev(rxg_ctx *ctx);
@@ -294,10 +309,17 @@ typedef struct rxg_handoff_ops {
 } rxg_handoff_ops;
 
 /* Performs, in packet order, the side effects ether_in() would have performed for
-   pkts[0..n) given their records.  frames[i] = the frame bytes of mbufs[i].  The
-   composition rxg_rx_burst + rxg_rx_replay equals `for (i<n) ether_in(mbufs[i])` when
-   no handler in the batch mutates the TCB table; handlers that do must mirror their
-   writes with rxg_tcb_* (see INTEGRATION.md). */
+   pkts[0..n) given their records.  frames[i] = the frame bytes of mbufs[i].  It must
+   follow the burst (rxg_rx_burst or rxg_rx_burst_dev) of the same batch on this context;
+   for rxg_rx_burst_dev the batch's device buffers must stay valid until it returns.
+
+   Sequential equivalence: handlers (tcpswitch[], send_reset, ...) mirror their writes to
+   tcbs[] with rxg_tcb_* as they happen.  When a handler changes the mirror, every later
+   TCP packet of the batch whose classification can depend on the change (same dport as a
+   changed slot; any packet that reached findtcb pass 2 after a slot was removed or NULL
+   slots appeared) is re-classified on the GPU against the updated table before it is
+   replayed, and the counters are corrected.  The composition rxg_rx_burst + rxg_rx_replay
+   therefore equals `for (i<n) ether_in(mbufs[i])`. */
 int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
 

@@ -1,0 +1,204 @@
+"""GPU: rxg_rx_burst + rxg_rx_replay equals the reference's sequential ether_in loop when the
+state handlers change the TCB table inside a burst.
+
+The handlers below mimic the kinds of writes tcp_states.c makes — tcp_listen allocates a
+child TCB carrying the SYN's tuple (tcp_states.c:150-207), tcp_syn_rcv moves it to
+ESTABLISHED, a FIN closes a flow and tcp_closed removes its slot (:209-219) — and mirror
+each write with rxg_tcb_*.  The expected result is the oracle run ONE packet at a time
+against the table as it stands when that packet is reached."""
+import ctypes as C
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import pktgen
+import rxg
+
+pytestmark = pytest.mark.gpu
+LISTENING, SYN_RECV, ESTABLISHED, CLOSED = 1, 3, 4, 0
+
+
+class Model:
+    """Table rows + the handler logic, applied identically to the python rows and rxg."""
+
+    def __init__(self, rows, eng=None):
+        self.rows = list(rows)
+        self.eng = eng
+
+    def _upsert(self, idx, row):
+        while len(self.rows) <= idx:
+            self.rows.append(None)
+        self.rows[idx] = row
+        if self.eng:
+            self.eng.tcb_upsert(idx, row[0], row[1], row[2] & 0xFFFFFFFF, row[3] & 0xFFFFFFFF, row[4])
+
+    def handle(self, idx, state, frame):
+        flags = frame[47]
+        sport = (frame[34] << 8) | frame[35]
+        src = int.from_bytes(frame[26:30], "big")
+        if state == LISTENING:          # tcp_listen: child at Ntcb with the SYN's tuple
+            lst = self.rows[idx]
+            self._upsert(len(self.rows), (lst[0], sport, lst[2], src, SYN_RECV))
+        elif state == SYN_RECV:         # tcp_syn_rcv -> ESTABLISHED
+            r = self.rows[idx]
+            self.rows[idx] = r[:4] + (ESTABLISHED,)
+            if self.eng:
+                self.eng.tcb_set_state(idx, ESTABLISHED)
+        elif state == ESTABLISHED and flags & 1:   # FIN: close
+            r = self.rows[idx]
+            self.rows[idx] = r[:4] + (CLOSED,)
+            if self.eng:
+                self.eng.tcb_set_state(idx, CLOSED)
+        elif state == CLOSED:           # tcp_closed: remove_tcb
+            self.rows[idx] = None
+            if self.eng:
+                self.eng.tcb_remove(idx)
+
+
+def scenario(seed, nflows=40, n=1500):
+    rng = random.Random(seed)
+    dst = pktgen.ip4(192, 168, 78, 2)
+    rows = [(80, 0, pktgen.raw_of_host(dst), 0, LISTENING)]
+    flows = []
+    for f in range(nflows):
+        src = pktgen.ip4(10, 1, f >> 8, f & 255)
+        rows.append((80, 2000 + f, pktgen.raw_of_host(dst), src, ESTABLISHED))
+        flows.append((src, 2000 + f))
+    rows.append((8080, 0, pktgen.raw_of_host(dst), 0, LISTENING))
+    clients = [(pktgen.ip4(172, 16, 0, c), 40000 + c) for c in range(60)]
+    frames = []
+    for _ in range(n):
+        k = rng.random()
+        if k < 0.35:
+            src, sport = rng.choice(flows)
+            fl = 0x11 if rng.random() < 0.05 else 0x10
+        else:
+            src, sport = rng.choice(clients)
+            fl = rng.choice([0x02, 0x10, 0x10, 0x18, 0x11])
+        dport = 8080 if rng.random() < 0.1 else 80
+        frames.append(pktgen.frame(src_ip=src, dst_ip=dst, sport=sport, dport=dport, flags=fl,
+                                   seq=rng.getrandbits(32), ack=rng.getrandbits(32),
+                                   payload=rng.randbytes(rng.randrange(0, 200))))
+    return rows, frames
+
+
+def sequential_reference(rows, frames):
+    """The reference loop: classify packet i against the table as it is NOW, then run its
+    handler.  Returns per-packet (verdict, tcb_idx, state) and the summed counters."""
+    m = Model(rows)
+    out, cnt = [], np.zeros(16, dtype=np.uint64)
+    for f in frames:
+        arena, off, lens = pktgen.pack_arena([f])
+        tcb, live = pktgen.table_arrays(m.rows)
+        rec, c = oracle.rx_batch(arena, off, lens, tcb, live)
+        cnt += c
+        r = rec[0]["c"]
+        out.append((int(r["verdict"]), int(r["tcb_idx"]), int(r["state"])))
+        if r["verdict"] == rxg.V_DISPATCH:
+            m.handle(int(r["tcb_idx"]), int(r["state"]), f)
+    return out, cnt, m.rows
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_replay_sequential_equivalence(engine, seed):
+    rows, frames = scenario(seed)
+    exp, ecnt, erows = sequential_reference(rows, frames)
+    tcb, live = pktgen.table_arrays(rows)
+    engine.tcb_load(tcb, live)
+    engine.tcb_sync()
+    engine.counters_reset()
+    recs = engine.rx_burst(frames, rxg.REC16)
+    model = Model(rows, engine)
+    bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
+    addr = {C.addressof(b): i for i, b in enumerate(bufs)}
+    got = [None] * len(frames)
+
+    def free_mbuf(u, m):
+        i = addr[m]
+        if got[i] is None:
+            got[i] = ("free",)
+    def rst(u, ip, tcp):
+        got[addr[ip - 14]] = ("rst",)
+    def tcpswitch(u, idx, st, tcp, ip, m):
+        i = addr[m]
+        got[i] = ("switch", idx, st)
+        model.handle(idx, st, frames[i])
+        return 0
+
+    ops = rxg.HandoffOps(None, rxg.HANDOFF_FREE(free_mbuf), rxg.HANDOFF_ARP_IN(), rxg.HANDOFF_GET_MAC(),
+                         rxg.HANDOFF_ADD_MAC(), rxg.HANDOFF_SEND_RESET(rst), rxg.HANDOFF_ON_SEGMENT(),
+                         rxg.HANDOFF_TCPSWITCH(tcpswitch))
+    ptrs = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
+    lib = rxg.load_library()
+    rc = lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, len(bufs), 16)
+    assert rc == 0, lib.rxg_last_error()
+    for i, (v, idx, st) in enumerate(exp):
+        if v == rxg.V_DISPATCH:
+            assert got[i] == ("switch", idx, st), (i, got[i], exp[i])
+        elif v in (rxg.V_RST_NOPCB, rxg.V_RST_LISTEN_NONSYN):
+            assert got[i] == ("rst",), (i, got[i], exp[i])
+    assert model.rows == erows
+    assert engine.counters().tolist() == ecnt.tolist()
+    # the burst alone (snapshot semantics) would have differed: the scenario bites
+    snap = [(int(r["verdict"]), int(r["tcb_idx"]), int(r["state"])) for r in recs]
+    assert snap != exp
+
+
+def test_arp_learn_flag_and_replay(engine):
+    """ip.c:30-32 with the ARP mirror: the burst flags TCP packets from unknown sources and
+    the replay calls add_mac once per new address, in first-seen order, never get_mac."""
+    rng = random.Random(9)
+    known = [pktgen.ip4(10, 0, 0, k) for k in range(20)]
+    unknown = [pktgen.ip4(10, 9, 0, k) for k in range(30)]
+    frames = []
+    for _ in range(800):
+        k = rng.random()
+        if k < 0.1:   # ARP and non-TCP frames never learn
+            frames.append(pktgen.frame(proto=17, src_ip=rng.choice(unknown)))
+            continue
+        src = rng.choice(known if k < 0.5 else unknown)
+        frames.append(pktgen.frame(src_ip=src, sport=rng.randrange(65536), flags=0x10))
+    tcb, live = pktgen.table_arrays([(80, 0, pktgen.raw_of_host(pktgen.ip4(192, 168, 78, 2)), 0, 1)])
+    engine.tcb_load(tcb, live)
+    engine.arp_load(known)
+    recs = engine.rx_burst(frames, rxg.REC16)
+    # flag: TCP and source not in the mirror at burst time
+    for f, r in zip(frames, recs):
+        is_tcp = r["verdict"] in (0, 1, 2)
+        src = int.from_bytes(f[26:30], "big")
+        assert bool(r["flags"] & rxg.F_ARP_LEARN) == (is_tcp and src not in known)
+    # reference order of add_mac: first TCP sighting of each unknown source
+    exp, seen = [], set(known)
+    for f, r in zip(frames, recs):
+        if r["verdict"] in (0, 1, 2):
+            src = int.from_bytes(f[26:30], "big")
+            if src not in seen:
+                seen.add(src)
+                exp.append(src)
+    calls = []
+
+    def add_mac(u, ip, mac):
+        calls.append(ip)
+        engine.arp_learned(ip)   # the integration's add_mac hook
+        return 1
+
+    def get_mac(u, ip, out):
+        raise AssertionError("get_mac walked while the ARP mirror is enabled")
+
+    bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
+    ops = rxg.HandoffOps(None, rxg.HANDOFF_FREE(), rxg.HANDOFF_ARP_IN(), rxg.HANDOFF_GET_MAC(get_mac),
+                         rxg.HANDOFF_ADD_MAC(add_mac), rxg.HANDOFF_SEND_RESET(), rxg.HANDOFF_ON_SEGMENT(),
+                         rxg.HANDOFF_TCPSWITCH())
+    ptrs = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
+    lib = rxg.load_library()
+    assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, len(bufs), 16) == 0
+    assert calls == exp
+    assert engine.arp_count() == len(known) + len(exp)
+    # a second burst of the same frames learns nothing new
+    recs2 = engine.rx_burst(frames, rxg.REC16)
+    assert not (recs2["flags"] & rxg.F_ARP_LEARN).any()
+    engine.arp_disable()
+    recs3 = engine.rx_burst(frames, rxg.REC16)
+    assert not (recs3["flags"] & rxg.F_ARP_LEARN).any()
