@@ -157,21 +157,22 @@ __device__ __forceinline__ Fields unpark_fields(const uint32_t *sf, int lane)
     return F;
 }
 
+// Loads are issued unconditionally (a chunk outside the frame reads the frame's first
+// chunk, or the arena's first bytes for an empty frame, and is then zeroed): with
+// predicated loads hipcc zero-initialises their destination registers and inserts
+// s_waitcnt between consecutive loads, serialising them.
 template <int LPF, int NLOAD, bool NT>
 __device__ __forceinline__ void load_chunks(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                             int lane, uint32_t (&d)[NLOAD][4])
 {
     const int gl = lane & (LPF - 1);
-    const uint8_t *fp = a.frames + (size_t)off * 64u;
+    const uint8_t *fp = (active && len) ? a.frames + (size_t)off * 64u : a.frames;
 #pragma unroll
     for (int j = 0; j < NLOAD; ++j) {
         const int c = gl + j * LPF;
-        if (active && (uint32_t)(c * 16) < len) {
-            uint4 v = load16<NT>(fp + c * 16);
-            d[j][0] = v.x; d[j][1] = v.y; d[j][2] = v.z; d[j][3] = v.w;
-        } else {
-            d[j][0] = d[j][1] = d[j][2] = d[j][3] = 0u;
-        }
+        const bool ok = active && (uint32_t)(c * 16) < len;
+        const uint4 v = load16<NT>(ok ? fp + c * 16 : fp);
+        d[j][0] = ok ? v.x : 0u; d[j][1] = ok ? v.y : 0u; d[j][2] = ok ? v.z : 0u; d[j][3] = ok ? v.w : 0u;
     }
 }
 
@@ -363,9 +364,41 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
 // Phase B: lane i classifies frame i of the slice (all 64 probes in flight together) and
 // writes its record; the records of a slice are one contiguous 1 KiB / 3 KiB store.
 // STRIP (experiment builds only): 1 = no frame loads, 2 = no TCB probe, 4 = no record store
+// First bucket of the exact-tuple probe, loaded early so that several frames' probes of
+// one lane are in flight together.
+struct Probe {
+    uint4 s0, s1, s2, s3;
+    uint32_t hb;
+};
+
+__device__ __forceinline__ Probe probe_issue(const RxArgs &a, bool valid, const Fields &F)
+{
+    Probe P;
+    const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
+    const bool is_tcp = valid && et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
+    P.hb = tuple_hash(F.ports, F.dst, bswap32(F.src)) & a.t.bucket_mask;
+    // always a valid bucket: load unconditionally (see load_chunks), use only for TCP
+    const uint4 *b = a.t.buckets + (size_t)P.hb * kSlotsPerBucket;
+    P.s0 = b[0]; P.s1 = b[1]; P.s2 = b[2]; P.s3 = b[3];
+    (void)is_tcp;
+    return P;
+}
+
+template <int MODE, int STRIP = 0>
+__device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
+                                                const Fields &F, const Probe &P, WaveCounters &wc);
+
 template <int MODE, int STRIP = 0>
 __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
                                                const Fields &F, WaveCounters &wc)
+{
+    const Probe P = probe_issue(a, valid && !(STRIP & 2), F);
+    classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc);
+}
+
+template <int MODE, int STRIP>
+__device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
+                                                const Fields &F, const Probe &P, WaveCounters &wc)
 {
     const uint32_t ck = valid ? F.ck : 0u, w_et = valid ? F.et : 0u, ports = valid ? F.ports : 0u;
     const uint32_t src_raw = valid ? F.src : 0u, dst_raw = valid ? F.dst : 0u, w_tl = valid ? F.tl : 0u;
@@ -396,10 +429,13 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     bool lhit = false, nslot = false;
     uint32_t st = RXG_STATE_NONE;
     if (is_tcp && !(STRIP & 2)) {
-        uint32_t hb = tuple_hash(ports, dst_raw, src_host) & a.t.bucket_mask;
+        uint32_t hb = P.hb;
+        uint4 s0 = P.s0, s1 = P.s1, s2 = P.s2, s3 = P.s3;
         for (uint32_t probe = 0; probe <= a.t.bucket_mask; ++probe) {
-            const uint4 *b = a.t.buckets + (size_t)hb * kSlotsPerBucket;
-            const uint4 s0 = b[0], s1 = b[1], s2 = b[2], s3 = b[3];
+            if (probe) {
+                const uint4 *b = a.t.buckets + (size_t)hb * kSlotsPerBucket;
+                s0 = b[0]; s1 = b[1]; s2 = b[2]; s3 = b[3];
+            }
             uint32_t v = kEmpty;
             if (s0.x == ports && s0.y == dst_raw && s0.z == src_host && s0.w != kEmpty) v = s0.w;
             if (s1.x == ports && s1.y == dst_raw && s1.z == src_host && s1.w != kEmpty) v = s1.w;
@@ -486,23 +522,27 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
 }
 
 // An all-small slice (64 frames of <= 64 bytes): lane l loads chunk l&3 of frame 16j + l/4
-// (instruction j covers 16 whole frames, 1 KiB, coalesced), writes it to the wave's LDS
-// at [frame][chunk], and after a wave barrier lane i reads back frame i's 64 bytes.
+// (instruction j covers 16 whole frames, 1 KiB, coalesced) ...
 template <bool NT>
-__device__ __forceinline__ void load_small_slice(const RxArgs &a, uint32_t off, uint32_t len, int lane,
-                                                 uint32_t *sf, uint32_t (&d)[4][4])
+__device__ __forceinline__ void issue_small_slice(const RxArgs &a, uint32_t off, uint32_t len, int lane,
+                                                  uint4 (&v)[4])
 {
-    uint4 v[4];
     const int ch = lane & 3;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int fr = 16 * j + (lane >> 2);
         const uint32_t foff = lane_read(off, fr), flen = lane_read(len, fr);
-        if ((uint32_t)(ch * 16) < flen)
-            v[j] = load16<NT>(a.frames + (size_t)foff * 64u + ch * 16);
-        else
-            v[j] = make_uint4(0u, 0u, 0u, 0u);
+        const bool ok = (uint32_t)(ch * 16) < flen;  // frames <= 64 B: a whole 64-B slot
+        const uint4 q = load16<NT>(ok ? a.frames + (size_t)foff * 64u + ch * 16 : a.frames);
+        v[j] = ok ? q : make_uint4(0u, 0u, 0u, 0u);
     }
+}
+
+// ... writes it to the wave's LDS at [frame][chunk], and after a wave barrier lane i reads
+// back frame i's 64 bytes.
+__device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int lane, uint32_t *sf,
+                                                      uint32_t (&d)[4][4])
+{
     uint4 *t = reinterpret_cast<uint4 *>(sf);
 #pragma unroll
     for (int j = 0; j < 4; ++j) t[j * 64 + lane] = v[j];  // [frame 16j + l/4][chunk l&3]
@@ -517,19 +557,21 @@ __device__ __forceinline__ void load_small_slice(const RxArgs &a, uint32_t off, 
     __builtin_amdgcn_wave_barrier();  // reads done before the LDS is reused
 }
 
+template <bool SEL>
 __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane, uint32_t &off, uint32_t &len)
 {
+    // unconditional (clamped) loads, invalid lanes zeroed afterwards: see load_chunks
     const uint32_t f = s * 64u + (uint32_t)lane;
-    off = 0u;
-    len = 0u;
-    if (s < ((a.n + 63u) >> 6) && f < a.n) {
-        const uint32_t pf = a.sel ? a.sel[f] : f;
-        off = a.off64[pf];
-        len = a.len[pf];
-    }
+    const bool ok = s < ((a.n + 63u) >> 6) && f < a.n;
+    const uint32_t fc = ok ? f : 0u;
+    const uint32_t pf = SEL ? a.sel[fc] : fc;
+    const uint32_t o = a.off64[pf];
+    const uint32_t l = a.len[pf];
+    off = ok ? o : 0u;
+    len = ok ? l : 0u;
 }
 
-template <int MODE, int CMASK, bool NT, bool PIPE = false, int STRIP = 0, bool SMALL_COALESCED = true>
+template <int MODE, int CMASK, bool NT, bool PAIR = false, int STRIP = 0, bool SEL = false>
 __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 {
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -554,8 +596,8 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     // loads are always in flight while slice s is processed.
     uint32_t s = wave;
     uint32_t c_off = 0, c_len = 0, n_off = 0, n_len = 0;
-    load_desc(a, s, lane, c_off, c_len);
-    load_desc(a, s + nwaves, lane, n_off, n_len);
+    load_desc<SEL>(a, s, lane, c_off, c_len);
+    load_desc<SEL>(a, s + nwaves, lane, n_off, n_len);
     while (s < nslices) {
         const uint32_t f = s * 64u + (uint32_t)lane;
         const bool valid = f < a.n;
@@ -563,41 +605,36 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         const int cls = valid ? size_class(len) : 9;
         if constexpr (MODE != 0 && (CMASK & 1)) {
             if (__ballot(cls == 0) == ~0ull) {
-                // All-small pipeline: every frame of the slice is <= 64 bytes, lane i owns
-                // frame i end to end (fields stay in registers), and the NEXT all-small
-                // slice's frame loads are issued before this slice is classified.
-                uint32_t d[4][4], e[4][4];
-                uint32_t cur_len = len;
-                if constexpr (STRIP & 1) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-#pragma unroll
-                        for (int w = 0; w < 4; ++w) d[j][w] = (uint32_t)lane * 0x01000193u + j + w;
-                } else if constexpr (SMALL_COALESCED) {
-                    load_small_slice<false>(a, off, cur_len, lane, sf, d);
-                } else {
-                    load_chunks<1, 4, false>(a, off, cur_len, true, lane, d);
+                // All-small slices: every frame <= 64 bytes; lane i owns frame i end to end
+                // (fields stay in registers).  Two such slices (s and s + nwaves) are done
+                // together when both are all-small: both slices' loads, then both probes,
+                // are in flight at once (one latency chain for two slices).
+                const uint32_t s2 = s + nwaves;
+                const bool pair = PAIR && __ballot(s2 < nslices && s2 * 64u + (uint32_t)lane < a.n &&
+                                                   n_len <= 64u) == ~0ull;
+                uint4 vA[4], vB[4];
+                issue_small_slice<false>(a, c_off, c_len, lane, vA);
+                if (pair) issue_small_slice<false>(a, n_off, n_len, lane, vB);
+                uint32_t x_off = n_off, x_len = n_len, y_off = 0, y_len = 0;
+                if (pair) load_desc<SEL>(a, s + 2u * nwaves, lane, x_off, x_len);
+                load_desc<SEL>(a, s + (pair ? 3u : 2u) * nwaves, lane, y_off, y_len);
+                uint32_t dA[4][4], dB[4][4];
+                transpose_small_slice(vA, lane, sf, dA);
+                const Fields FA = frame_fields<1, 4, false, MODE, false>(a, c_off, c_len, true, lane, dA);
+                Fields FB = FA;
+                if (pair) {
+                    transpose_small_slice(vB, lane, sf, dB);
+                    FB = frame_fields<1, 4, false, MODE, false>(a, n_off, n_len, true, lane, dB);
                 }
-                for (;;) {
-                    const uint32_t s2 = s + nwaves;
-                    const uint32_t f2 = s2 * 64u + (uint32_t)lane;
-                    const bool small2 = PIPE && __ballot(s2 < nslices && f2 < a.n && n_len <= 64u) == ~0ull;
-                    if (small2) load_chunks<1, 4, false>(a, n_off, n_len, true, lane, e);
-                    uint32_t nn_off = 0, nn_len = 0;
-                    load_desc(a, s2 + nwaves, lane, nn_off, nn_len);
-                    const Fields F = frame_fields<1, 4, false, MODE, false>(a, c_off, cur_len, true, lane, d);
-                    classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, cur_len, F, wc);
-                    bytes += cur_len;
-                    s = s2;
-                    c_off = n_off; c_len = n_len;
-                    n_off = nn_off; n_len = nn_len;
-                    if (!small2) break;
-                    cur_len = c_len;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-#pragma unroll
-                        for (int w = 0; w < 4; ++w) d[j][w] = e[j][w];
+                classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, FA, wc);
+                bytes += c_len;
+                if (pair) {
+                    classify_store<MODE, STRIP>(a, s2 * 64u + (uint32_t)lane, true, n_len, FB, wc);
+                    bytes += n_len;
                 }
+                s += (pair ? 2u : 1u) * nwaves;
+                c_off = x_off; c_len = x_len;
+                n_off = y_off; n_len = y_len;
                 continue;
             }
         }
@@ -623,7 +660,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         }
         s += nwaves;
         c_off = n_off; c_len = n_len;
-        load_desc(a, s + nwaves, lane, n_off, n_len);
+        load_desc<SEL>(a, s + nwaves, lane, n_off, n_len);
     }
 
     if (a.counters == nullptr) return;
@@ -779,20 +816,19 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     // L.variant: experiment builds only (a class subset; frames of other classes are skipped)
     // production kernels use non-temporal loads for the >256 B classes (measured +5 %
     // at 1500 B, -4 % at 64 B: classes 0-2 always use plain loads)
+    if (L.sel) {  // re-classification of selected frames (rxg_rx_replay), records of 16 B
+        hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (L.mode == 16) {
-        switch (L.variant) {
+        switch (L.variant) {  // experiment variants (RXG_VARIANT); 0 = production
         case 1: hipLaunchKernelGGL((rx_kernel<16, 0x01, false>), dim3(blocks), dim3(256), 0, st, a); break;
         case 2: hipLaunchKernelGGL((rx_kernel<16, 0x20, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 3: hipLaunchKernelGGL((rx_kernel<16, 0xFF, false>), dim3(blocks), dim3(256), 0, st, a); break;
         case 4: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 5: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 6: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 1>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 7: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 2>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 8: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 4>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 9: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 6>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 10: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 7>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 11: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, false>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 12: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, false, 0, false>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 6: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 7: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         default: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
     } else if (L.mode == 48) {

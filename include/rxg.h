@@ -231,7 +231,9 @@ int rxg_arp_disable(rxg_ctx *ctx);
 
 /* Device-resident batch.  Frame i occupies bytes [frames + 64*off64[i],
    + len[i]); the bytes up to the next 64-byte boundary must be readable
-   (their contents are ignored).  len[i] = rte_pktmbuf_data_len(m). */
+   (their contents are ignored), and so must the first 64 bytes at `frames`
+   (loads for chunks outside a frame are redirected there, then discarded).
+   len[i] = rte_pktmbuf_data_len(m). */
 typedef struct rxg_dev_batch {
     const void *frames;     /* dev */
     const uint32_t *off64;  /* dev, n entries, in 64-byte units */

@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")]
 import rxg  # noqa: E402
 
-WL = {"c3": (1500, 1000, 0, 1), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3)}
+WL = {"c3": (1500, 1000, 0, 1), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3),
+      "c2r1": (64, 1, 0, 1), "c2x4": (64, 1, 0, 4)}
 
 
 def main():
@@ -27,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--frames-c2", type=int, default=0, help="override frames for c2* workloads")
     ap.add_argument("--rec", type=int, default=16)
     args = ap.parse_args()
 
@@ -34,12 +36,13 @@ def main():
     wls = {}
     for w in args.workloads.split(","):
         L, flows, mix, copies = WL[w]
-        bs = [base.synth(n=args.frames, nflows=flows, len_a=L or 1500, mix=mix, seed=77 + c)
+        nfr = args.frames_c2 if (w.startswith("c2") and args.frames_c2) else args.frames
+        bs = [base.synth(n=nfr, nflows=flows, len_a=L or 1500, mix=mix, seed=77 + c)
               for c in range(copies)]
-        lens = bs[0]["len"].download(np.uint16, args.frames)
+        lens = bs[0]["len"].download(np.uint16, nfr)
         tcb, live = rxg.synthetic_tcb_table(flows)
-        wls[w] = (bs, int(lens.astype(np.uint64).sum()), tcb, live)
-    out = base.alloc(args.frames * args.rec)
+        wls[w] = (bs, int(lens.astype(np.uint64).sum()), tcb, live, nfr)
+    out = base.alloc(max(args.frames, args.frames_c2) * args.rec)
     base.sync()
 
     engines = {}
@@ -51,18 +54,18 @@ def main():
         engines[v] = rxg.Engine(0)
     res = {(v, w): [] for v in engines for w in wls}
     for r in range(args.rounds):
-        for w, (bs, nbytes, tcb, live) in wls.items():
+        for w, (bs, nbytes, tcb, live, nfr) in wls.items():
             for v, eng in engines.items():
                 eng.tcb_load(tcb, live)
                 eng.tcb_sync()
                 evs = [(eng.event(), eng.event()) for _ in range(args.iters)]
                 for i in range(2):
                     b = bs[i % len(bs)]
-                    eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, args.frames, out.ptr, args.rec)
+                    eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, nfr, out.ptr, args.rec)
                 for i in range(args.iters):
                     b = bs[(i + 2) % len(bs)]
                     eng.record(evs[i][0])
-                    eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, args.frames, out.ptr, args.rec)
+                    eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, nfr, out.ptr, args.rec)
                     eng.record(evs[i][1])
                 eng.sync()
                 ms = [eng.elapsed_ms(a, b) for a, b in evs]
