@@ -74,7 +74,7 @@ def max_over_ranks(x: float, device) -> float:
 def barrier(device):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
-    if device.type == "cuda":
+    if torch.cuda.is_available():
         torch.cuda.synchronize()
 
 
@@ -289,12 +289,16 @@ def main():
     args = ap.parse_args()
 
     rank, world, local = rank_env()
+    # RXG_BENCH_REHEARSE=1: rehearse N ranks on fewer GPUs (device = local_rank mod #GPUs,
+    # gloo backend for the collectives) -- a correctness rehearsal, never a measurement.
+    rehearse = os.environ.get("RXG_BENCH_REHEARSE") == "1"
+    gpu = local % max(1, torch.cuda.device_count()) if rehearse else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(local)
-    eng = rxg.Engine(device=local)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
+    device = torch.device("cpu") if (rehearse and world > 1) else torch.device("cuda", gpu)
+    torch.cuda.set_device(gpu)
+    eng = rxg.Engine(device=gpu)
     stream = None  # the engine's own stream
 
     seed = shard_seed(0x5EED0001, rank)
