@@ -18,7 +18,7 @@ import sys
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librxg.so")
+LIB_PATH = os.environ.get("RXG_LIB") or os.path.join(_HERE, "librxg.so")
 
 # ---------------------------------------------------------------- constants (rxg.h) ---
 ETHER_TYPE_IPV4 = 0x0800

@@ -1,4 +1,4 @@
 set -u
-mkdir -p gpurun_out/r01n
-export RXG_BENCH_REHEARSE=1
-timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/r01n/bench2.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/r01n/bench2.log | tail -5; echo "rc=$rc"
+O=$PWD/dpdk-tcpipstack_amd/rxg/librxg_old.so
+timeout -k 10 300 python -m pytest tests -m gpu -x -q 2>&1 | tail -3 &&
+timeout -k 10 500 python scripts/kbench.py --variants 0:0::$O,0:0,0:1024,0:1152 --workloads c3,c4,c2 --rounds 4 2>&1 | grep -v amdgpu.ids

@@ -45,17 +45,28 @@ def main():
     out = base.alloc(max(args.frames, args.frames_c2) * args.rec)
     base.sync()
 
-    engines = {}
+    # A variant may name another build of librxg (4th field, a path): A/B of two builds in
+    # one process.  The binding's module-level library handle is switched per engine.
+    main_lib = rxg.load_library()
+    libs, engines = {}, {}
     for v in args.variants.split(","):
         parts = v.split(":")
         os.environ["RXG_VARIANT"] = parts[0]
         os.environ["RXG_MAX_BLOCKS"] = parts[1]
         os.environ["RXG_NOCOUNT"] = "1" if (len(parts) > 2 and parts[2] == "nc") else "0"
+        lib = main_lib
+        if len(parts) > 3 and parts[3]:
+            rxg._lib = None
+            lib = rxg.load_library(parts[3])
+        rxg._lib = lib
+        libs[v] = lib
         engines[v] = rxg.Engine(0)
+        rxg._lib = main_lib
     res = {(v, w): [] for v in engines for w in wls}
     for r in range(args.rounds):
         for w, (bs, nbytes, tcb, live, nfr) in wls.items():
             for v, eng in engines.items():
+                rxg._lib = libs[v]
                 eng.tcb_load(tcb, live)
                 eng.tcb_sync()
                 evs = [(eng.event(), eng.event()) for _ in range(args.iters)]
@@ -71,8 +82,9 @@ def main():
                 ms = [eng.elapsed_ms(a, b) for a, b in evs]
                 res[(v, w)].append(float(np.median(ms)))
                 for a, b in evs:
-                    rxg.load_library().rxg_event_destroy(eng.ctx, a)
-                    rxg.load_library().rxg_event_destroy(eng.ctx, b)
+                    libs[v].rxg_event_destroy(eng.ctx, a)
+                    libs[v].rxg_event_destroy(eng.ctx, b)
+                rxg._lib = main_lib
     for (v, w), ms in res.items():
         nbytes = wls[w][1]
         med = float(np.median(ms))
