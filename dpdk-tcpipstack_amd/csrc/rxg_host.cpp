@@ -86,7 +86,20 @@ struct rxg_ctx {
     const uint32_t *last_off = nullptr;
     const uint16_t *last_len = nullptr;
     uint32_t last_n = 0;
+    const uint8_t *last_recs = nullptr;  // the burst's records (device) and their size
+    uint32_t last_stride = 0;
     DevBuf d_sel, d_fix;
+
+    // payload hand-off: receive-window mirror (0 unknown, 1 no pairs, 2 pairs pending) and
+    // the gathered burst's message descriptors (pinned host copy)
+    std::vector<uint32_t> rcv_cur;
+    std::vector<uint8_t> rcv_state;
+    DevBuf d_pg_scratch;
+    rxg_payload_msg *h_pm = nullptr;
+    uint32_t h_pm_cap = 0, pm_n = 0;
+    bool pm_pending = false;
+    hipEvent_t pm_ev = nullptr;
+    int64_t replay_pos = -1;  // packet whose handlers rxg_rx_replay is running
 
     // ARP mirror (host set + device open-addressing table)
     bool arp_enabled = false, arp_dirty = false;
@@ -198,8 +211,10 @@ extern "C" int rxg_fini(rxg_ctx *c)
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp})
+    for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_scratch})
         if (b->p) (void)hipFree(b->p);
+    if (c->h_pm) (void)hipHostFree(c->h_pm);
+    if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
     if (c->counters) (void)hipFree(c->counters);
     if (c->h_arena) (void)hipHostFree(c->h_arena);
     if (c->h_off) (void)hipHostFree(c->h_off);
@@ -260,6 +275,7 @@ extern "C" int rxg_tcb_remove(rxg_ctx *c, int32_t idx)
     if (c->live[idx]) c->touched.push_back(c->tcb[idx].dport);
     c->touched_pass2 = true;
     c->live[idx] = 0;
+    if ((size_t)idx < c->rcv_state.size()) c->rcv_state[idx] = 0;  // FreeWindow
     c->dirty = true;
     c->gen++;
     return 0;
@@ -293,6 +309,8 @@ extern "C" int rxg_tcb_load(rxg_ctx *c, const rxg_tcb_tuple *tcbs, const uint8_t
     c->dirty = true;
     c->touched_all = true;
     c->gen++;
+    c->rcv_cur.clear();
+    c->rcv_state.clear();
     return 0;
 }
 
@@ -458,6 +476,9 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
     c->last_off = b->off64;
     c->last_len = b->len;
     c->last_n = b->n;
+    c->last_recs = (const uint8_t *)b->out;
+    c->last_stride = b->rec_kind;
+    c->pm_n = 0;  // a gather describes the burst it followed
     // the records reflect the mirror as of now: changes are tracked from here (replay)
     c->touched.clear();
     c->touched_all = c->touched_pass2 = false;
@@ -541,6 +562,86 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
     return 0;
 }
 
+// ----------------------------------------------------------------- payload hand-off ---
+extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void *stream)
+{
+    if (!c || !o) return fail(-EINVAL, "rxg_payload_gather_dev: NULL argument");
+    if (!c->last_frames || !c->last_recs)
+        return fail(-EINVAL, "rxg_payload_gather_dev: no burst to gather from");
+    const uint32_t n = c->last_n;
+    if (n && (!o->msgs || !o->arena_used || (o->arena_cap && !o->arena)))
+        return fail(-EINVAL, "rxg_payload_gather_dev: NULL output buffer");
+    int rc = set_device(c);
+    if (rc) return rc;
+    hipStream_t st = pick(c, stream);
+    if ((rc = ensure(c->d_pg_scratch, (size_t)payload_blocks(n) * sizeof(unsigned long long)))) return rc;
+    LaunchPayload P;
+    P.frames = c->last_frames;
+    P.off64 = c->last_off;
+    P.len = c->last_len;
+    P.recs = c->last_recs;
+    P.stride = c->last_stride;
+    P.n = n;
+    P.msgs = o->msgs;
+    P.arena = (uint8_t *)o->arena;
+    P.arena_cap = o->arena ? o->arena_cap : 0;
+    P.scratch = (unsigned long long *)c->d_pg_scratch.p;
+    P.used = (unsigned long long *)o->arena_used;
+    HIP_OK(launch_payload(P, st));
+    // the descriptors rxg_payload_take consults, copied behind the gather
+    if (n > c->h_pm_cap) {
+        if (c->h_pm) HIP_OK(hipHostFree(c->h_pm));
+        c->h_pm = nullptr;
+        c->h_pm_cap = 0;
+        HIP_OK(hipHostMalloc((void **)&c->h_pm, (size_t)n * sizeof(rxg_payload_msg), hipHostMallocDefault));
+        c->h_pm_cap = n;
+    }
+    if (!c->pm_ev) HIP_OK(hipEventCreateWithFlags(&c->pm_ev, hipEventDisableTiming));
+    if (n) HIP_OK(hipMemcpyAsync(c->h_pm, o->msgs, (size_t)n * sizeof(rxg_payload_msg), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipEventRecord(c->pm_ev, st));
+    c->pm_n = n;
+    c->pm_pending = true;
+    return 0;
+}
+
+extern "C" int rxg_rcv_set(rxg_ctx *c, int32_t idx, uint32_t cur_seq, uint32_t pairs_pending)
+{
+    if (!c) return fail(-EINVAL, "rxg_rcv_set: ctx NULL");
+    if (idx < 0 || idx >= kMaxTcbs) return fail(-EINVAL, "rxg_rcv_set: index %d", idx);
+    if ((size_t)idx >= c->rcv_state.size()) {
+        c->rcv_state.resize((size_t)idx + 1, 0);
+        c->rcv_cur.resize((size_t)idx + 1, 0);
+    }
+    c->rcv_cur[idx] = cur_seq;
+    c->rcv_state[idx] = pairs_pending ? 2 : 1;
+    return 0;
+}
+
+// PushData (tcp_windows.c:341-358) with an empty SeqPairs list and
+// CurrentSequenceNumber == seq: the out-of-window test needs SeqPairs (:345) and is
+// skipped; the duplicate test (:349) drops iff cur > seq + Length (u32); AdjustPair puts
+// the one pair at the head (:42-110, returns seq + Length + FIN); GetData pops it with
+// offset 0 and copies Length bytes (:158-180) -> one message of exactly this payload.
+extern "C" int rxg_payload_take(rxg_ctx *c, int32_t idx, uint32_t seq, uint32_t length, rxg_payload_msg *msg)
+{
+    if (!c) return fail(-EINVAL, "rxg_payload_take: ctx NULL");
+    const int64_t pos = c->replay_pos;
+    if (pos < 0 || (uint64_t)pos >= c->pm_n || length == 0 || length > 0xFFFFu) return 0;
+    if (c->pm_pending) {
+        HIP_OK(hipEventSynchronize(c->pm_ev));
+        c->pm_pending = false;
+    }
+    const rxg_payload_msg &m = c->h_pm[pos];
+    if (!(m.flags & RXG_PM_GATHERED) || m.len != length) return 0;
+    if (idx < 0 || (size_t)idx >= c->rcv_state.size() || c->rcv_state[idx] != 1 || c->rcv_cur[idx] != seq)
+        return 0;
+    if (seq > (uint32_t)(seq + length)) return 0;  // the duplicate test drops it
+    if (seq == 0) return 0;  // GetData asserts CurrentSequenceNumber != 0 (:151): the stack's own code
+    c->rcv_cur[idx] = seq + length;
+    if (msg) *msg = m;
+    return 1;
+}
+
 // ----------------------------------------------------------------------- counters ---
 extern "C" int rxg_counters_reset(rxg_ctx *c, void *stream)
 {
@@ -620,6 +721,10 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         return fail(-EINVAL, "rxg_rx_replay: NULL argument");
     if (stride != RXG_REC16 && stride != RXG_REC48) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
     if (n && c->last_n != n) return fail(-EINVAL, "rxg_rx_replay: n=%u but the last burst had %u frames", n, c->last_n);
+    struct PosGuard {
+        rxg_ctx *c;
+        ~PosGuard() { c->replay_pos = -1; }
+    } pos_guard{c};
     std::vector<rxg_rec16> cur(n);
     for (uint32_t i = 0; i < n; ++i) cur[i] = *(const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
     std::vector<uint8_t> stale(n, 0);
@@ -665,6 +770,7 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
             }
         }
         const rxg_rec16 &r = cur[i];
+        c->replay_pos = i;  // rxg_payload_take answers for this packet
         void *m = mbufs[i];
         uint8_t *f = (uint8_t *)frames[i];
         void *ip = f + RXG_OFF_IP, *tcp = f + RXG_OFF_TCP;

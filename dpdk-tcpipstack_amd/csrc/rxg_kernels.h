@@ -30,7 +30,24 @@ struct LaunchSynth {
     uint32_t n, nflows, dst_ip, dport, mix, len_a;
 };
 
+struct LaunchPayload {
+    const uint8_t *frames;
+    const uint32_t *off64;
+    const uint16_t *len;
+    const uint8_t *recs;   // the burst's records (rxg_rec16 / rxg_rec48, `stride` bytes apart)
+    uint32_t stride;
+    uint32_t n;
+    rxg_payload_msg *msgs;
+    uint8_t *arena;
+    uint64_t arena_cap;
+    unsigned long long *scratch;  // payload_blocks(n) entries
+    unsigned long long *used;     // 1 entry
+};
+
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
+// rxg_payload.hip: gather of the burst's candidate payloads (three launches)
+hipError_t launch_payload(const LaunchPayload &P, hipStream_t st);
+uint32_t payload_blocks(uint32_t n);
 // resident 256-thread workgroups per CU of the production kernel of `mode`
 int rx_blocks_per_cu(int mode);
 hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);

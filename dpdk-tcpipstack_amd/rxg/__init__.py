@@ -47,6 +47,8 @@ REC48_DTYPE = np.dtype([("c", REC16_DTYPE), ("ether_type", "<u2"), ("sport", "<u
                         ("seq", "<u4"), ("ack", "<u4"), ("src_ip", "<u4"),
                         ("dst_ip_raw", "<u4"), ("data_off", "u1"), ("src_mac", "u1", (6,)),
                         ("reserved", "u1")])
+PM_GATHERED, PM_REF_OVERSIZE = 0x01, 0x02
+PAYLOAD_MSG_DTYPE = np.dtype([("arena_off", "<u8"), ("len", "<u4"), ("flags", "<u4")])
 TCB_DTYPE = np.dtype([("dport", "<i4"), ("sport", "<i4"), ("ipv4_dst", "<u4"),
                       ("ipv4_src", "<u4"), ("state", "u1"), ("pad", "u1"),
                       ("identifier", "<u2")])
@@ -82,6 +84,15 @@ class DevTxBatch(C.Structure):
 class PktView(C.Structure):
     _fields_ = [("buf_addr", C.c_void_p), ("data_off", C.c_uint16), ("data_len", C.c_uint16),
                 ("pad", C.c_uint32)]
+
+
+class PayloadMsg(C.Structure):
+    _fields_ = [("arena_off", C.c_uint64), ("len", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class PayloadOut(C.Structure):
+    _fields_ = [("arena", C.c_void_p), ("arena_cap", C.c_uint64), ("msgs", C.c_void_p),
+                ("arena_used", C.c_void_p)]
 
 
 class SynthParams(C.Structure):
@@ -151,6 +162,9 @@ def load_library(path: str = LIB_PATH):
         "rxg_counters_read": (C.c_int, [vp, vp]),
         "rxg_counters_dev": (vp, [vp]),
         "rxg_rx_replay": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, vp, u32, u32]),
+        "rxg_payload_gather_dev": (C.c_int, [vp, C.POINTER(PayloadOut), vp]),
+        "rxg_rcv_set": (C.c_int, [vp, i32, u32, u32]),
+        "rxg_payload_take": (C.c_int, [vp, i32, u32, u32, C.POINTER(PayloadMsg)]),
         "rxg_synth_dev": (C.c_int, [vp, C.POINTER(SynthParams), vp, u64, vp, vp, vp,
                                     C.POINTER(u64), vp]),
         "rxg_synth_arena_bytes": (u64, [C.POINTER(SynthParams)]),
@@ -416,6 +430,36 @@ class Engine:
         _check(_lib.rxg_rx_burst(self.ctx, views, n, rec_kind, _ptr(out) if n else None),
                "rxg_rx_burst")
         return out
+
+    # --- payload hand-off
+    def payload_gather_dev(self, arena: int, arena_cap: int, msgs: int, used: int, stream=None):
+        o = PayloadOut(arena, arena_cap, msgs, used)
+        _check(_lib.rxg_payload_gather_dev(self.ctx, C.byref(o), stream), "rxg_payload_gather_dev")
+
+    def payload_gather(self, n: int, arena_cap: int):
+        """Gather the last burst's payloads; returns (arena bytes, msgs, bytes needed)."""
+        da, dm, du = self.alloc(max(arena_cap, 16)), self.alloc(max(n, 1) * 16), self.alloc(8)
+        try:
+            self.payload_gather_dev(da.ptr, arena_cap, dm.ptr, du.ptr)
+            self.sync()
+            msgs = dm.download(PAYLOAD_MSG_DTYPE, n) if n else np.zeros(0, PAYLOAD_MSG_DTYPE)
+            used = int(du.download(np.uint64, 1)[0])
+            arena = da.download(np.uint8, min(arena_cap, used)) if arena_cap else np.zeros(0, np.uint8)
+            return arena, msgs, used
+        finally:
+            for d in (da, dm, du):
+                d.free()
+
+    def rcv_set(self, idx: int, cur_seq: int, pairs_pending: bool):
+        _check(_lib.rxg_rcv_set(self.ctx, idx, cur_seq & 0xFFFFFFFF, int(bool(pairs_pending))),
+               "rxg_rcv_set")
+
+    def payload_take(self, idx: int, seq: int, length: int):
+        """Inside a replay handler: (True, arena_off) if the gathered payload is the message."""
+        m = PayloadMsg()
+        rc = _lib.rxg_payload_take(self.ctx, idx, seq & 0xFFFFFFFF, length, C.byref(m))
+        _check(min(rc, 0), "rxg_payload_take")
+        return rc == 1, int(m.arena_off)
 
     # --- counters
     def counters_reset(self, stream=None):

@@ -326,6 +326,62 @@ int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
 
 /* ------------------------------------------------------------------------- */
+/* Payload hand-off.  The reference copies each       */
+/* in-order segment's payload into a mempool message for the socket ring:     */
+/* tcp_established -> PushData (tcp_windows.c:341-358) -> AdjustPair (:42-110) */
+/* -> PushDataInQueue (:112-136) -> GetData (:138-186).  rxg gathers the      */
+/* payloads of a whole burst on the device; during rxg_rx_replay the stack's  */
+/* PushData asks rxg_payload_take whether the window would deliver exactly    */
+/* that payload as one message, and uses the gathered bytes if so.            */
+/* ------------------------------------------------------------------------- */
+enum rxg_payload_flag {
+    RXG_PM_GATHERED = 0x01,     /* arena holds this frame's payload                          */
+    RXG_PM_REF_OVERSIZE = 0x02  /* len >= 1000: the reference's GetData asserts here
+                                   (tcp_windows.c:170, its Buffer[1000]); rxg delivers it   */
+};
+
+typedef struct rxg_payload_msg {
+    uint64_t arena_off;  /* payload at arena + arena_off, 16-byte aligned                    */
+    uint32_t len;        /* Length = datalen (tcp_states.c:111), bytes at frame + 34 +
+                            (data_off >> 4) * 4 (tcp_windows.c:164-166); 0 if not gathered   */
+    uint32_t flags;      /* RXG_PM_*                                                        */
+} rxg_payload_msg;
+
+typedef struct rxg_payload_out {
+    void *arena;             /* dev; each message padded with zeros to 16 bytes             */
+    uint64_t arena_cap;      /* bytes                                                       */
+    rxg_payload_msg *msgs;   /* dev, one per frame of the burst (flags 0: not gathered)      */
+    uint64_t *arena_used;    /* dev, 1 entry: bytes the burst's candidates need; frames past
+                                arena_cap are not gathered                                  */
+} rxg_payload_out;
+
+/* Gathers, for the LAST burst on this context (rxg_rx_burst or rxg_rx_burst_dev; its
+   device batch and records must still be valid), the payload of every TCP segment
+   (verdict DISPATCH, RST_NOPCB or RST_LISTEN_NONSYN -- the replay may turn the latter into
+   a DISPATCH) with datalen > 0 and the payload inside the frame.  Packet order;
+   asynchronous on `stream`.  Also queues a copy of the message
+   descriptors to the host for rxg_payload_take. */
+int rxg_payload_gather_dev(rxg_ctx *ctx, const rxg_payload_out *o, void *stream);
+
+/* Receive-window mirror: ReceiveWindow.CurrentSequenceNumber of tcbs[idx] and whether its
+   SeqPairs list is non-empty (tcp_windows.h:37-44).  The stack calls it wherever it
+   writes them itself: tcp_listen (tcp_states.c:182) and after its own PushData when
+   rxg_payload_take refused.  rxg_tcb_remove / rxg_tcb_load forget the slot's window. */
+int rxg_rcv_set(rxg_ctx *ctx, int32_t idx, uint32_t cur_seq, uint32_t pairs_pending);
+
+/* Called from the stack's PushData(mbuf, tcp, Length, ptcb) (tcp_windows.c:341) while
+   rxg_rx_replay runs the handlers of a packet of the gathered burst.  Returns 1 when the
+   reference would deliver exactly this packet's payload as one message -- the mirror says
+   the window of tcbs[idx] holds no pairs and CurrentSequenceNumber == seq, the payload was
+   gathered with this length, and PushData's duplicate test (cur > seq + Length, u32) does
+   not drop it.  Then *msg describes the message, the mirror advances to seq + Length, and
+   the stack does what AdjustPair + GetData + PushDataInQueue would have: ptcb->ack =
+   seq + Length + (FIN ? 1 : 0), CurrentSequenceNumber = seq + Length, enqueue a message of
+   Length bytes (the gathered ones), free the mbuf.  Returns 0 otherwise (the stack runs its
+   own PushData, then rxg_rcv_set); negative on error. */
+int rxg_payload_take(rxg_ctx *ctx, int32_t idx, uint32_t seq, uint32_t length, rxg_payload_msg *msg);
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic traffic (bench / tests): Eth + IPv4 (IHL 5) + TCP (doff 5, ACK)   */
 /* frames with valid checksums, SURVEY.md §8(d).                               */
 /* ------------------------------------------------------------------------- */
