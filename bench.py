@@ -235,6 +235,37 @@ def c5_leg(eng, n, steps, warmup, device, seed):
     return res
 
 
+def payload_leg(eng, wl, steps, warmup):
+    """the device payload gather (rxg_payload_gather_dev) after a burst
+    of the workload.  Algorithmic bytes per launch = 2 x payload bytes (read + write) + 16 B
+    record read + 16 B descriptor write per frame; HIP events around the three launches."""
+    wl.launch(eng, 0)
+    pl = (wl.lens.astype(np.int64) - 54).clip(min=0)  # synthetic frames: IHL 5, data_off 5
+    dl = int(pl.sum())
+    cap = int(((pl + 15) // 16 * 16).sum())
+    arena, msgs, used = eng.alloc(cap), eng.alloc(wl.n * 16), eng.alloc(8)
+    try:
+        for _ in range(warmup):
+            eng.payload_gather_dev(arena.ptr, cap, msgs.ptr, used.ptr)
+        evs = [(eng.event(), eng.event()) for _ in range(steps)]
+        for a, b in evs:
+            eng.record(a)
+            eng.payload_gather_dev(arena.ptr, cap, msgs.ptr, used.ptr)
+            eng.record(b)
+        eng.sync()
+        ms = [eng.elapsed_ms(a, b) for a, b in evs]
+        k = float(np.mean(ms)) / 1e3
+        alg = 2 * dl + 32 * wl.n
+        assert int(used.download(np.uint64, 1)[0]) == cap
+        return {"payload_bytes": dl, "arena_bytes": cap,
+                "kernels_us": round(k * 1e6, 2), "achieved_GBps": round(alg / k / 1e9, 1),
+                "roofline_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_launch": alg}
+    finally:
+        for d in (arena, msgs, used):
+            d.free()
+
+
 def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
     """The oracle's faithful restatement of the reference rx path (port), on one host
     core, over a bounded sample of the same workload (first sample_n frames)."""
@@ -345,6 +376,7 @@ def main():
                                     and int(c2[7]) == 0 and int(c2[8]) == 0),
             }
             lw.free()
+        legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)
         legs["c5_bidir_copy_inclusive"] = c5_leg(eng, args.frames, max(3, args.steps // 4), 1, device,
                                                  seed)

@@ -61,6 +61,7 @@ struct rxg_ctx {
     uint32_t grid_rec16 = 0, grid_rec48 = 0, grid_tx = 0;
     int variant = 0;  // RXG_VARIANT: experiment kernels (tools/kbench only)
     int nocount = 0;  // RXG_NOCOUNT: experiment only, skip the counter reduction
+    int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather experiment kernels
 
     // host mirror of tcbs[0..ntcb)
     std::vector<rxg_tcb_tuple> tcb;
@@ -94,10 +95,13 @@ struct rxg_ctx {
     // the gathered burst's message descriptors (pinned host copy)
     std::vector<uint32_t> rcv_cur;
     std::vector<uint8_t> rcv_state;
-    DevBuf d_pg_scratch;
+    DevBuf d_pg_status, d_pg_ticket;
+    unsigned long long pg_tickets = 0;  // workgroups the gathers have launched so far
+    uint32_t pg_epoch = 0;
     rxg_payload_msg *h_pm = nullptr;
+    const rxg_payload_msg *d_pm = nullptr;  // the gather's descriptors (device)
     uint32_t h_pm_cap = 0, pm_n = 0;
-    bool pm_pending = false;
+    bool pm_pending = false;  // h_pm not fetched yet for this gather
     hipEvent_t pm_ev = nullptr;
     int64_t replay_pos = -1;  // packet whose handlers rxg_rx_replay is running
 
@@ -176,6 +180,7 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     }
     if (const char *v = getenv("RXG_VARIANT")) c->variant = atoi(v);
     if (const char *v = getenv("RXG_NOCOUNT")) c->nocount = atoi(v);
+    if (const char *v = getenv("RXG_PG_VARIANT")) c->pg_variant = atoi(v);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(-EIO, "rxg_init: hipStreamCreate failed");
@@ -211,7 +216,7 @@ extern "C" int rxg_fini(rxg_ctx *c)
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_scratch})
+    for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket})
         if (b->p) (void)hipFree(b->p);
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
@@ -574,7 +579,17 @@ extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void
     int rc = set_device(c);
     if (rc) return rc;
     hipStream_t st = pick(c, stream);
-    if ((rc = ensure(c->d_pg_scratch, (size_t)payload_blocks(n) * sizeof(unsigned long long)))) return rc;
+    const uint32_t nb = payload_blocks(n);
+    const void *old_status = c->d_pg_status.p;
+    if ((rc = ensure(c->d_pg_status, (size_t)nb * sizeof(unsigned long long)))) return rc;
+    if (c->d_pg_status.p != old_status)  // fresh memory: no word may look published
+        HIP_OK(hipMemsetAsync(c->d_pg_status.p, 0, c->d_pg_status.bytes, st));
+    if (!c->d_pg_ticket.p) {
+        if ((rc = ensure(c->d_pg_ticket, sizeof(unsigned long long)))) return rc;
+        HIP_OK(hipMemsetAsync(c->d_pg_ticket.p, 0, sizeof(unsigned long long), st));
+        c->pg_tickets = 0;
+    }
+    c->pg_epoch = (c->pg_epoch % ((1u << 30) - 1u)) + 1u;
     LaunchPayload P;
     P.frames = c->last_frames;
     P.off64 = c->last_off;
@@ -585,20 +600,19 @@ extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void
     P.msgs = o->msgs;
     P.arena = (uint8_t *)o->arena;
     P.arena_cap = o->arena ? o->arena_cap : 0;
-    P.scratch = (unsigned long long *)c->d_pg_scratch.p;
+    P.status = (unsigned long long *)c->d_pg_status.p;
+    P.ticket = (unsigned long long *)c->d_pg_ticket.p;
+    P.ticket_base = c->pg_tickets;
     P.used = (unsigned long long *)o->arena_used;
-    HIP_OK(launch_payload(P, st));
-    // the descriptors rxg_payload_take consults, copied behind the gather
-    if (n > c->h_pm_cap) {
-        if (c->h_pm) HIP_OK(hipHostFree(c->h_pm));
-        c->h_pm = nullptr;
-        c->h_pm_cap = 0;
-        HIP_OK(hipHostMalloc((void **)&c->h_pm, (size_t)n * sizeof(rxg_payload_msg), hipHostMallocDefault));
-        c->h_pm_cap = n;
-    }
+    P.epoch = c->pg_epoch;
+    P.variant = c->pg_variant;
+    uint32_t tickets = 0;
+    HIP_OK(launch_payload(P, st, &tickets));
+    c->pg_tickets += tickets;
+    // rxg_payload_take fetches the descriptors on its first call after this gather
     if (!c->pm_ev) HIP_OK(hipEventCreateWithFlags(&c->pm_ev, hipEventDisableTiming));
-    if (n) HIP_OK(hipMemcpyAsync(c->h_pm, o->msgs, (size_t)n * sizeof(rxg_payload_msg), hipMemcpyDeviceToHost, st));
     HIP_OK(hipEventRecord(c->pm_ev, st));
+    c->d_pm = o->msgs;
     c->pm_n = n;
     c->pm_pending = true;
     return 0;
@@ -627,8 +641,18 @@ extern "C" int rxg_payload_take(rxg_ctx *c, int32_t idx, uint32_t seq, uint32_t 
     if (!c) return fail(-EINVAL, "rxg_payload_take: ctx NULL");
     const int64_t pos = c->replay_pos;
     if (pos < 0 || (uint64_t)pos >= c->pm_n || length == 0 || length > 0xFFFFu) return 0;
-    if (c->pm_pending) {
+    if (c->pm_pending) {  // first take after the gather: fetch the burst's descriptors
         HIP_OK(hipEventSynchronize(c->pm_ev));
+        if (c->pm_n > c->h_pm_cap) {
+            if (c->h_pm) HIP_OK(hipHostFree(c->h_pm));
+            c->h_pm = nullptr;
+            c->h_pm_cap = 0;
+            HIP_OK(hipHostMalloc((void **)&c->h_pm, (size_t)c->pm_n * sizeof(rxg_payload_msg), hipHostMallocDefault));
+            c->h_pm_cap = c->pm_n;
+        }
+        HIP_OK(hipMemcpyAsync(c->h_pm, c->d_pm, (size_t)c->pm_n * sizeof(rxg_payload_msg), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
         c->pm_pending = false;
     }
     const rxg_payload_msg &m = c->h_pm[pos];

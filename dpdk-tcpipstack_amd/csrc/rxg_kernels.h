@@ -40,13 +40,17 @@ struct LaunchPayload {
     rxg_payload_msg *msgs;
     uint8_t *arena;
     uint64_t arena_cap;
-    unsigned long long *scratch;  // payload_blocks(n) entries
-    unsigned long long *used;     // 1 entry
+    unsigned long long *status;       // payload_blocks(n) look-back words (any content)
+    unsigned long long *ticket;       // workgroup ticket counter, kept across launches
+    unsigned long long ticket_base;   // its value before this launch
+    unsigned long long *used;         // 1 entry
+    uint32_t epoch;                   // 1 .. 2^30-1, new for every launch on `status`
+    int variant;                      // 0 = production; >0 experiment variants (RXG_PG_VARIANT)
 };
 
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
-// rxg_payload.hip: gather of the burst's candidate payloads (three launches)
-hipError_t launch_payload(const LaunchPayload &P, hipStream_t st);
+// rxg_payload.hip: gather of the burst's candidate payloads (one launch + a memset)
+hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *tickets_used);
 uint32_t payload_blocks(uint32_t n);
 // resident 256-thread workgroups per CU of the production kernel of `mode`
 int rx_blocks_per_cu(int mode);

@@ -7,13 +7,16 @@
 // as 20 bytes whatever the IHL, like the parse).  rxg does that copy for a whole burst in
 // three launches:
 //
-//   pg_sizes   per 1024-frame block: the bytes of its candidate payloads (each rounded up
-//              to 16 so that every message starts 16-byte aligned in the arena);
-//   pg_scan    one workgroup: exclusive scan of the block totals (= block offsets);
-//   pg_copy    per block: in-block scan -> per-frame message descriptors, then 16-lane
-//              groups copy the payloads (source misaligned by 54 mod 16 for a 20-byte TCP
-//              header: 16-byte loads + a cross-lane byte funnel shift; destination 16-byte
-//              aligned, the tail of the last chunk zeroed).
+//   pg_gather  ONE launch, 256 frames per workgroup: each workgroup sums its candidates'
+//              arena space (each payload rounded up to 16 bytes so that every message starts
+//              16-byte aligned), finds its offset by a decoupled look-back over the
+//              workgroups before it (virtual workgroup ids from an atomic ticket, so every
+//              workgroup it waits for is running; each status word is an epoch-tagged
+//              64-bit {flag, value} granule, the data being its own flag), writes the
+//              message descriptors, then each wave copies its 64 frames' payloads one
+//              16-byte destination chunk per lane (source misaligned by 54 mod 16 for a
+//              20-byte TCP header: 16-byte loads + a cross-lane byte funnel shift;
+//              destination 16-byte aligned, the tail of the last chunk zeroed).
 //
 // A candidate is every TCP segment of the burst (verdict DISPATCH, RST_NOPCB or
 // RST_LISTEN_NONSYN: the replay may re-classify the latter two to a DISPATCH when a
@@ -29,12 +32,11 @@
 namespace rxg {
 namespace {
 
-constexpr int kPgThreads = 256;
-constexpr int kPgPerThread = 4;
-constexpr int kPgPerBlock = kPgThreads * kPgPerThread;  // frames per block
-constexpr int kG = 16;                                  // lanes per payload in the copy
-constexpr int kU = 4;                                   // 16-byte chunks per lane per round
-constexpr int kScanThreads = 1024;
+constexpr int kPgThreads = 256;  // = frames per workgroup
+constexpr int kMaxU = 4;         // copy rounds in flight per wave (max)
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 struct PgArgs {
     const uint8_t *frames;
@@ -46,8 +48,11 @@ struct PgArgs {
     rxg_payload_msg *msgs;
     uint8_t *arena;
     uint64_t arena_cap;
-    unsigned long long *block_off;  // nblocks entries: totals, then (pg_scan) offsets
-    unsigned long long *used;       // 1 entry: arena bytes the burst needs
+    unsigned long long *status;  // per virtual workgroup: epoch << 34 | flag << 32 | value/16
+    unsigned long long *ticket;  // virtual workgroup ids, counting across launches
+    unsigned long long ticket_base;
+    unsigned long long *used;    // 1 entry: arena bytes the burst needs (~0: look-back timed out)
+    uint32_t epoch;              // 30 bits, never 0
     uint32_t nblocks;
 };
 
@@ -57,7 +62,6 @@ struct Cand {
     uint32_t flags;
 };
 
-__device__ __forceinline__ uint64_t round16(uint32_t x) { return ((uint64_t)x + 15u) & ~15ull; }
 
 __device__ __forceinline__ Cand candidate(const PgArgs &a, uint32_t i)
 {
@@ -91,50 +95,6 @@ __device__ __forceinline__ T wave_incl_scan(T v, int lane)
     return v;
 }
 
-__global__ __launch_bounds__(kPgThreads) void pg_sizes(PgArgs a)
-{
-    __shared__ unsigned long long s_w[kPgThreads / 64];
-    const uint32_t base = blockIdx.x * (uint32_t)kPgPerBlock;
-    unsigned long long s = 0;
-#pragma unroll
-    for (int k = 0; k < kPgPerThread; ++k) s += round16(candidate(a, base + threadIdx.x + k * kPgThreads).len);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-    if (lane == 0) s_w[w] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int k = 0; k < kPgThreads / 64; ++k) t += s_w[k];
-        a.block_off[blockIdx.x] = t;
-    }
-}
-
-// One workgroup: block totals -> exclusive block offsets (in place); *used = the sum.
-__global__ __launch_bounds__(kScanThreads) void pg_scan(PgArgs a)
-{
-    __shared__ unsigned long long s_w[kScanThreads / 64];
-    const uint32_t per = (a.nblocks + kScanThreads - 1) / kScanThreads;
-    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, a.nblocks);
-    unsigned long long s = 0;
-    for (uint32_t b = b0; b < b1; ++b) s += a.block_off[b];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const unsigned long long incl = wave_incl_scan(s, lane);
-    if (lane == 63) s_w[w] = incl;
-    __syncthreads();
-    unsigned long long wo = 0;
-    for (int k = 0; k < w; ++k) wo += s_w[k];
-    unsigned long long run = wo + incl - s;
-    for (uint32_t b = b0; b < b1; ++b) {
-        const unsigned long long t = a.block_off[b];
-        a.block_off[b] = run;
-        run += t;
-    }
-    if (threadIdx.x == kScanThreads - 1) *a.used = run;
-}
-
-__device__ __forceinline__ uint4 ld16(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
-
 __device__ __forceinline__ uint4 bperm16(uint4 v, int src_lane)
 {
     uint4 r;
@@ -167,108 +127,309 @@ __device__ __forceinline__ uint32_t keep_bytes(uint32_t v, int nb)
     return nb >= 4 ? v : nb <= 0 ? 0u : (v & ((1u << (8 * nb)) - 1u));
 }
 
-// One payload by a group of kG lanes (j = lane in the group, gb = the group's first lane
-// in the wave).  Destination chunk k (16 bytes) = source bytes [16k + sh, 16k + sh + 16)
-// from the 16-byte-aligned source chunks k and k + 1.  Lane j loads chunk k = k0 + u*kG + j
-// and takes chunk k + 1 from lane j + 1 (lane kG-1: from lane 0's next u, or its own extra
-// load after the last u).
-__device__ __forceinline__ void copy_payload(const PgArgs &a, uint64_t src, uint64_t dst, uint32_t L, int j,
-                                             int gb)
+// Copy phase of pg_copy: lane-per-chunk.  A wave takes its 256 frames in batches of 64;
+// the batch's payloads (compacted, in packet order) form one run of T destination chunks
+// of 16 bytes, and round r gives lane l chunk 64r + l.  The payload a chunk belongs to is
+// found without a search: the payloads' first chunks of the round are marked in a 64-entry
+// LDS array, a ballot turns the marks into a mask, and a popcount below the lane counts
+// the payloads started so far.  kU rounds are in flight per iteration.  Destination chunk
+// k of a payload = source bytes [16k + sh, 16k + sh + 16) from the 16-byte-aligned source
+// chunks k and k + 1; chunk k + 1 comes from the next lane when that lane copies the same
+// payload, else from a load of its own.
+struct WaveCopy {
+    uint64_t src[64];   // compacted payloads of the batch: source byte offset in frames,
+    uint64_t dst[64];   // destination byte offset in the arena,
+    uint32_t start[64]; // first destination chunk within the batch's run,
+    uint32_t len[64];   // bytes
+    uint32_t head[64 * kMaxU];
+};
+
+template <bool NT>
+__device__ __forceinline__ uint4 ldp(const uint8_t *p)
 {
-    const uint8_t *s0 = a.frames + (src & ~15ull);
-    const uint32_t sh = (uint32_t)(src & 15u);
-    const uint32_t nsrc = (sh + L + 15u) >> 4, ndst = (L + 15u) >> 4;
-    uint8_t *d0 = a.arena + dst;
-    const int next_lane = (j == kG - 1) ? gb : gb + j + 1;
-    for (uint32_t k0 = 0; k0 < ndst; k0 += kG * kU) {
-        uint4 A[kU];
+    if constexpr (NT) {
+        typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+        const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ void stp(uint8_t *p, uint4 o)
+{
+    if constexpr (NT) {
+        typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+        v4 v;
+        v.x = o.x; v.y = o.y; v.z = o.z; v.w = o.w;
+        __builtin_nontemporal_store(v, reinterpret_cast<v4 *>(p));
+    } else {
+        *reinterpret_cast<uint4 *>(p) = o;
+    }
+}
+
+// One round of lanes in flight: lane's destination chunk k of compacted payload p, its
+// source chunk k, and chunk k + 1 when the next lane does not supply it (E).
+struct Round {
+    uint4 A, E;
+    uint32_t p, k;
+    bool act, own;
+};
+
+template <int kU, bool NT>
+__device__ __forceinline__ void issue_rounds(const PgArgs &a, WaveCopy &W, uint32_t r0, uint32_t T, bool valid,
+                                             uint32_t start, int lane, unsigned long long le, Round (&R)[kU])
+{
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint32_t k = k0 + u * kG + j;
-            const uint4 v = ld16(s0 + 16u * (k < nsrc ? k : 0u));
-            A[u] = k < nsrc ? v : make_uint4(0u, 0u, 0u, 0u);
-        }
-        uint4 E = make_uint4(0u, 0u, 0u, 0u);
-        if (j == kG - 1) {
-            const uint32_t k = k0 + kU * kG;
-            if (k < nsrc) E = ld16(s0 + 16u * k);
-        }
+    for (int u = 0; u < kU; ++u) W.head[64 * u + lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (valid && start >= r0 && start < r0 + 64u * kU) W.head[start - r0] = 1u;
+    __builtin_amdgcn_wave_barrier();
+    const int nl = lane == 63 ? 63 : lane + 1;
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint4 give = (j == 0 && u + 1 < kU) ? A[u + 1] : A[u];
-            uint4 N = bperm16(give, next_lane);
-            if (j == kG - 1 && u == kU - 1) N = E;
-            const uint32_t k = k0 + u * kG + j;
-            if (k < ndst) {
-                uint4 o = sh ? funnel16(A[u], N, sh) : A[u];
-                const int valid = (int)L - (int)(16u * k);
-                if (valid < 16) {
-                    o.x = keep_bytes(o.x, valid);
-                    o.y = keep_bytes(o.y, valid - 4);
-                    o.z = keep_bytes(o.z, valid - 8);
-                    o.w = keep_bytes(o.w, valid - 12);
-                }
-                *reinterpret_cast<uint4 *>(d0 + 16u * k) = o;
+    for (int u = 0; u < kU; ++u) {
+        const uint32_t base = r0 + 64u * u;
+        const unsigned long long mask = __ballot(W.head[64 * u + lane] != 0u);
+        const uint32_t before = (uint32_t)__popcll(__ballot(valid && start < base));
+        const uint32_t idx = base + (uint32_t)lane;
+        R[u].act = idx < T;
+        R[u].p = R[u].act ? before + (uint32_t)__popcll(mask & le) - 1u : 0u;
+        R[u].k = R[u].act ? idx - W.start[R[u].p] : 0u;
+        const uint64_t s = W.src[R[u].p];
+        const uint8_t *s0 = a.frames + (s & ~15ull);
+        R[u].A = ldp<NT>(s0 + 16u * R[u].k);
+        const uint32_t pn = (uint32_t)__builtin_amdgcn_ds_bpermute(nl << 2, (int)R[u].p);
+        R[u].own = lane == 63 || idx + 1u >= T || pn != R[u].p;
+        const uint32_t sh = (uint32_t)(s & 15u);
+        R[u].E = make_uint4(0u, 0u, 0u, 0u);
+        if (R[u].act && sh && R[u].own && R[u].k + 1u < ((sh + W.len[R[u].p] + 15u) >> 4))
+            R[u].E = ldp<NT>(s0 + 16u * (R[u].k + 1u));
+    }
+    __builtin_amdgcn_wave_barrier();  // head[] is rewritten by the next issue
+}
+
+template <int kU, bool NT>
+__device__ __forceinline__ void store_rounds(const PgArgs &a, const WaveCopy &W, int lane, const Round (&R)[kU])
+{
+    const int nl = lane == 63 ? 63 : lane + 1;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint4 N0 = bperm16(R[u].A, nl);
+        const uint4 N = R[u].own ? R[u].E : N0;
+        if (R[u].act) {
+            const uint64_t s = W.src[R[u].p];
+            const uint32_t sh = (uint32_t)(s & 15u), L = W.len[R[u].p];
+            uint4 o = sh ? funnel16(R[u].A, N, sh) : R[u].A;
+            const int vb = (int)L - (int)(16u * R[u].k);
+            if (vb < 16) {
+                o.x = keep_bytes(o.x, vb);
+                o.y = keep_bytes(o.y, vb - 4);
+                o.z = keep_bytes(o.z, vb - 8);
+                o.w = keep_bytes(o.w, vb - 12);
             }
+            stp<NT>(a.arena + W.dst[R[u].p] + 16u * R[u].k, o);
         }
     }
 }
 
-__global__ __launch_bounds__(kPgThreads) void pg_copy(PgArgs a)
+// The wave's 64 frames (lane = frame; L = 0: nothing to copy).  Software-pipelined: the
+// loads of the next kU rounds are issued before the current rounds are stored.
+template <int kU, bool NT>
+__device__ __forceinline__ void copy_batch(const PgArgs &a, WaveCopy &W, uint64_t src, uint64_t dst, uint32_t L,
+                                           int lane)
 {
-    __shared__ uint64_t s_src[kPgPerBlock];
-    __shared__ uint64_t s_dst[kPgPerBlock];
-    __shared__ uint32_t s_len[kPgPerBlock];
-    __shared__ unsigned long long s_w[kPgThreads / 64];
-    const uint32_t base = blockIdx.x * (uint32_t)kPgPerBlock;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-
-    // this thread's 4 consecutive frames, in packet order
-    Cand c[kPgPerThread];
-    unsigned long long mine = 0;
-#pragma unroll
-    for (int k = 0; k < kPgPerThread; ++k) {
-        c[k] = candidate(a, base + (uint32_t)(t * kPgPerThread + k));
-        mine += round16(c[k].len);
+    const bool valid = L != 0u;
+    const unsigned long long vm = __ballot(valid);
+    if (vm == 0ull) return;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
+    const uint32_t nch = valid ? (L + 15u) >> 4 : 0u;
+    const uint32_t incl = wave_incl_scan(nch, lane);
+    const uint32_t start = incl - nch;
+    const uint32_t T = (uint32_t)__shfl(incl, 63, 64);
+    if (valid) {
+        W.src[rank] = src;
+        W.dst[rank] = dst;
+        W.start[rank] = start;
+        W.len[rank] = L;
     }
-    const unsigned long long incl = wave_incl_scan(mine, lane);
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    constexpr uint32_t kStep = 64u * kU;
+    Round X[kU], Y[kU];
+    issue_rounds<kU, NT>(a, W, 0u, T, valid, start, lane, le, X);
+    uint32_t r0 = 0;
+    for (;;) {
+        const bool more = r0 + kStep < T;
+        if (more) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, Y);
+        store_rounds<kU, NT>(a, W, lane, X);
+        if (!more) break;
+        r0 += kStep;
+        const bool more2 = r0 + kStep < T;
+        if (more2) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, X);
+        store_rounds<kU, NT>(a, W, lane, Y);
+        if (!more2) break;
+        r0 += kStep;
+    }
+    __builtin_amdgcn_wave_barrier();  // W is rewritten by the next batch
+}
+
+// status word flags
+constexpr uint32_t kAgg = 1u, kIncl = 2u;
+
+__device__ __forceinline__ unsigned long long status_word(uint32_t epoch, uint32_t flag, uint32_t v16)
+{
+    return ((unsigned long long)epoch << 34) | ((unsigned long long)flag << 32) | v16;
+}
+
+// Wave 0 of workgroup vb: the exclusive prefix (16-byte units) of the workgroups before it.
+// Each poll covers 256 predecessors: lane l reads workgroups j - l - 64q (q < 4), distance
+// d = l + 64q.  Every word up to the nearest published inclusive prefix must be published
+// (aggregate or inclusive), else the wave polls again.
+__device__ __forceinline__ uint32_t look_back(const PgArgs &a, uint32_t vb, int lane, bool &timed_out)
+{
+    constexpr int kQ = 4;
+    uint32_t excl = 0;
+    int64_t j = (int64_t)vb - 1;
+    uint32_t spins = 0;
+    while (j >= 0) {
+        unsigned long long wd[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int64_t idx = j - lane - 64 * q;
+            wd[q] = status_word(a.epoch, kIncl, 0u);  // before workgroup 0
+            if (idx >= 0)
+                wd[q] = __hip_atomic_load((gu64 *)(a.status + idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        int first = 64 * kQ;  // distance of the nearest inclusive prefix
+        uint32_t flag[kQ];
+#pragma unroll
+        for (int q = kQ - 1; q >= 0; --q) {
+            flag[q] = (uint32_t)(wd[q] >> 34) == a.epoch ? (uint32_t)(wd[q] >> 32) & 3u : 0u;
+            const unsigned long long im = __ballot(flag[q] == kIncl);
+            if (im) first = 64 * q + __builtin_ctzll(im);
+        }
+        bool missing = false;
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const bool need = lane + 64 * q <= first;
+            missing |= need && flag[q] == 0u;
+            v += need ? (uint32_t)wd[q] : 0u;
+        }
+        if (__ballot(missing)) {
+            if (++spins > kSpinLimit) {
+                timed_out = true;
+                return 0u;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        excl += v;
+        if (first < 64 * kQ) break;
+        j -= 64 * kQ;
+    }
+    return excl;
+}
+
+// FPT frames per thread (workgroup = 256 * FPT frames, thread t owns frames FPT*t ..
+// FPT*t + FPT-1 for the scan; wave w copies frames [64 FPT w, 64 FPT (w+1)) 64 at a time).
+// TICKET: virtual workgroup ids from an atomic ticket (dispatch-order independent).
+template <int kU, bool NT, int FPT, bool TICKET>
+__global__ __launch_bounds__(kPgThreads) void pg_gather(PgArgs a)
+{
+    constexpr int FPB = kPgThreads * FPT;
+    __shared__ uint32_t s_vb, s_excl;
+    __shared__ uint32_t s_w[kPgThreads / 64];
+    __shared__ WaveCopy s_wc[kPgThreads / 64];
+    __shared__ uint64_t s_src[FPT > 1 ? FPB : 1];
+    __shared__ uint64_t s_dst[FPT > 1 ? FPB : 1];
+    __shared__ uint32_t s_len[FPT > 1 ? FPB : 1];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t vb = blockIdx.x;
+    if constexpr (TICKET) {
+        if (t == 0) s_vb = (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+        __syncthreads();
+        vb = s_vb;
+    }
+    const uint32_t i0 = vb * (uint32_t)FPB + (uint32_t)(t * FPT);
+
+    Cand c[FPT];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) {
+        c[k] = candidate(a, i0 + k);
+        mine += (c[k].len + 15u) >> 4;
+    }
+    const uint32_t incl = wave_incl_scan(mine, lane);
     if (lane == 63) s_w[w] = incl;
     __syncthreads();
-    unsigned long long off = a.block_off[blockIdx.x];
-    for (int k = 0; k < w; ++k) off += s_w[k];
-    off += incl - mine;
+    uint32_t agg = 0, wex = 0;
 #pragma unroll
-    for (int k = 0; k < kPgPerThread; ++k) {
-        const int q = t * kPgPerThread + k;
-        const uint32_t i = base + (uint32_t)q;
-        const uint64_t r16 = round16(c[k].len);
-        const bool fits = c[k].len != 0u && off + r16 <= a.arena_cap;
-        if (i < a.n) {
+    for (int k = 0; k < kPgThreads / 64; ++k) {
+        agg += s_w[k];
+        wex += k < w ? s_w[k] : 0u;
+    }
+    if (w == 0) {
+        if (lane == 0)
+            __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, vb ? kAgg : kIncl, agg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool timed_out = false;
+        const uint32_t excl = vb ? look_back(a, vb, lane, timed_out) : 0u;
+        if (lane == 0) {
+            if (vb)
+                __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, kIncl, excl + agg),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (timed_out) atomicMax(a.used, ~0ull);
+            else if (vb == a.nblocks - 1) atomicMax(a.used, (unsigned long long)(excl + agg) * 16ull);
+            s_excl = excl;
+        }
+    }
+    __syncthreads();
+    uint64_t off = ((uint64_t)s_excl + wex + incl - mine) * 16ull;
+    uint64_t dst[FPT];
+    uint32_t cl[FPT];
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) {
+        const uint64_t r = 16ull * ((c[k].len + 15u) >> 4);
+        const bool fits = c[k].len != 0u && off + r <= a.arena_cap;
+        if (i0 + k < a.n) {
             rxg_payload_msg m;
             m.arena_off = fits ? off : 0ull;
             m.len = fits ? c[k].len : 0u;
             m.flags = fits ? c[k].flags : 0u;
-            a.msgs[i] = m;
+            a.msgs[i0 + k] = m;
         }
-        s_src[q] = c[k].src;
-        s_dst[q] = off;
-        s_len[q] = fits ? c[k].len : 0u;
-        off += r16;
+        dst[k] = off;
+        cl[k] = fits ? c[k].len : 0u;
+        off += r;
     }
-    __syncthreads();
-
-    const int g = t / kG, j = t % kG, gb = lane & ~(kG - 1);
-    for (int q = g; q < kPgPerBlock; q += kPgThreads / kG) {
-        const uint32_t L = s_len[q];
-        if (L) copy_payload(a, s_src[q], s_dst[q], L, j, gb);
+    if constexpr (FPT == 1) {
+        copy_batch<kU, NT>(a, s_wc[w], c[0].src, dst[0], cl[0], lane);
+    } else {
+#pragma unroll
+        for (int k = 0; k < FPT; ++k) {
+            s_src[t * FPT + k] = c[k].src;
+            s_dst[t * FPT + k] = dst[k];
+            s_len[t * FPT + k] = cl[k];
+        }
+        __syncthreads();
+        for (int b = 0; b < FPT; ++b) {
+            const int q = w * 64 * FPT + b * 64 + lane;
+            copy_batch<kU, NT>(a, s_wc[w], s_src[q], s_dst[q], s_len[q], lane);
+        }
     }
 }
 
 }  // namespace
 
-hipError_t launch_payload(const LaunchPayload &P, hipStream_t st)
+// status words the launch may use (sized for the smallest workgroup)
+uint32_t payload_blocks(uint32_t n) { return (n + kPgThreads - 1) / kPgThreads; }
+
+hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *launched)
 {
-    if (P.n == 0) return hipMemsetAsync(P.used, 0, sizeof(unsigned long long), st);
     PgArgs a;
     a.frames = P.frames;
     a.off64 = P.off64;
@@ -279,15 +440,26 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st)
     a.msgs = P.msgs;
     a.arena = P.arena;
     a.arena_cap = P.arena_cap;
-    a.block_off = P.scratch;
+    a.status = P.status;
+    a.ticket = P.ticket;
+    a.ticket_base = P.ticket_base;
     a.used = P.used;
-    a.nblocks = payload_blocks(P.n);
-    hipLaunchKernelGGL(pg_sizes, dim3(a.nblocks), dim3(kPgThreads), 0, st, a);
-    hipLaunchKernelGGL(pg_scan, dim3(1), dim3(kScanThreads), 0, st, a);
-    hipLaunchKernelGGL(pg_copy, dim3(a.nblocks), dim3(kPgThreads), 0, st, a);
+    a.epoch = P.epoch;
+    *launched = 0;
+    hipError_t e = hipMemsetAsync(P.used, 0, sizeof(unsigned long long), st);
+    if (e != hipSuccess || P.n == 0) return e;
+    const int fpt = (P.variant == 6 || P.variant == 7) ? 4 : 1;
+    a.nblocks = (P.n + kPgThreads * fpt - 1) / (kPgThreads * fpt);
+    const dim3 g(a.nblocks), b(kPgThreads);
+    switch (P.variant) {  // experiment variants (RXG_PG_VARIANT); 0 = production
+    case 1: hipLaunchKernelGGL((pg_gather<4, false, 1, true>), g, b, 0, st, a); break;
+    case 5: hipLaunchKernelGGL((pg_gather<4, true, 1, false>), g, b, 0, st, a); break;
+    case 6: hipLaunchKernelGGL((pg_gather<4, true, 4, true>), g, b, 0, st, a); break;
+    case 7: hipLaunchKernelGGL((pg_gather<4, true, 4, false>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((pg_gather<4, true, 1, true>), g, b, 0, st, a);
+    }
+    *launched = (a.ticket && (P.variant != 5 && P.variant != 7)) ? a.nblocks : 0u;
     return hipGetLastError();
 }
-
-uint32_t payload_blocks(uint32_t n) { return (n + kPgPerBlock - 1) / kPgPerBlock; }
 
 }  // namespace rxg

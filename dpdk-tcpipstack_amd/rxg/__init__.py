@@ -306,6 +306,9 @@ class Engine:
 
     def close(self):
         if getattr(self, "ctx", None):
+            for d in getattr(self, "_pg_bufs", ()):
+                d.free()
+            self._pg_bufs = ()
             _lib.rxg_fini(self.ctx)
             self.ctx = None
 
@@ -437,18 +440,18 @@ class Engine:
         _check(_lib.rxg_payload_gather_dev(self.ctx, C.byref(o), stream), "rxg_payload_gather_dev")
 
     def payload_gather(self, n: int, arena_cap: int):
-        """Gather the last burst's payloads; returns (arena bytes, msgs, bytes needed)."""
+        """Gather the last burst's payloads; returns (arena bytes, msgs, bytes needed).  The
+        device buffers live until the next call (rxg_payload_take reads the descriptors)."""
+        for d in getattr(self, "_pg_bufs", ()):
+            d.free()
         da, dm, du = self.alloc(max(arena_cap, 16)), self.alloc(max(n, 1) * 16), self.alloc(8)
-        try:
-            self.payload_gather_dev(da.ptr, arena_cap, dm.ptr, du.ptr)
-            self.sync()
-            msgs = dm.download(PAYLOAD_MSG_DTYPE, n) if n else np.zeros(0, PAYLOAD_MSG_DTYPE)
-            used = int(du.download(np.uint64, 1)[0])
-            arena = da.download(np.uint8, min(arena_cap, used)) if arena_cap else np.zeros(0, np.uint8)
-            return arena, msgs, used
-        finally:
-            for d in (da, dm, du):
-                d.free()
+        self._pg_bufs = (da, dm, du)
+        self.payload_gather_dev(da.ptr, arena_cap, dm.ptr, du.ptr)
+        self.sync()
+        msgs = dm.download(PAYLOAD_MSG_DTYPE, n) if n else np.zeros(0, PAYLOAD_MSG_DTYPE)
+        used = int(du.download(np.uint64, 1)[0])
+        arena = da.download(np.uint8, min(arena_cap, used)) if arena_cap else np.zeros(0, np.uint8)
+        return arena, msgs, used
 
     def rcv_set(self, idx: int, cur_seq: int, pairs_pending: bool):
         _check(_lib.rxg_rcv_set(self.ctx, idx, cur_seq & 0xFFFFFFFF, int(bool(pairs_pending))),

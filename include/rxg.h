@@ -359,8 +359,8 @@ typedef struct rxg_payload_out {
    device batch and records must still be valid), the payload of every TCP segment
    (verdict DISPATCH, RST_NOPCB or RST_LISTEN_NONSYN -- the replay may turn the latter into
    a DISPATCH) with datalen > 0 and the payload inside the frame.  Packet order;
-   asynchronous on `stream`.  Also queues a copy of the message
-   descriptors to the host for rxg_payload_take. */
+   asynchronous on `stream`.  o->msgs must stay valid until the burst's replay is done:
+   the first rxg_payload_take after the gather copies the descriptors to the host. */
 int rxg_payload_gather_dev(rxg_ctx *ctx, const rxg_payload_out *o, void *stream);
 
 /* Receive-window mirror: ReceiveWindow.CurrentSequenceNumber of tcbs[idx] and whether its
