@@ -5,7 +5,7 @@
 # Usage: scripts/gpu_check.sh [tag] [steps...]   (steps default: all)
 set -u
 TAG=${1:-r01}; shift || true
-STEPS=${*:-"pytest smoke bench prof pmc"}
+STEPS=${*:-"pytest smoke bench prof pmc pgprof"}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -29,4 +29,8 @@ has bench && step bench 400 python bench.py
 has prof && step rocprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- $BENCH_PROF
 has pmc && step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rx_kernel -d "$OUT/pmc_fetch" -o run --output-format csv -- $BENCH_PROF
 has pmc && step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rx_kernel -d "$OUT/pmc_write" -o run --output-format csv -- $BENCH_PROF
+PG="python3 scripts/pgbench.py --workloads c3 --iters 10"
+has pgprof && step pg_rocprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/pg_prof" -o run --output-format csv -- $PG
+has pgprof && step pg_pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex pg_gather -d "$OUT/pg_pmc_fetch" -o run --output-format csv -- $PG
+has pgprof && step pg_pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex pg_gather -d "$OUT/pg_pmc_write" -o run --output-format csv -- $PG
 echo "=== done"
