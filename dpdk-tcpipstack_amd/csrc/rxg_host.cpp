@@ -567,6 +567,22 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
     return 0;
 }
 
+extern "C" int rxg_ether_in(rxg_ctx *c, const rxg_handoff_ops *ops, void *mbuf, void *frame, uint16_t data_len)
+{
+    if (!c || !ops || !frame) return fail(-EINVAL, "rxg_ether_in: NULL argument");
+    rxg_pkt_view v;
+    v.buf_addr = frame;
+    v.data_off = 0;
+    v.data_len = data_len;
+    v.pad = 0;
+    rxg_rec16 rec;
+    int rc = rxg_rx_burst(c, &v, 1, RXG_REC16, &rec);
+    if (rc) return rc;
+    void *m = mbuf, *f = frame;
+    rc = rxg_rx_replay(c, ops, &m, &f, &rec, 1, RXG_REC16);
+    return rc ? rc : 0;  // ether_in always returns 0 (etherin.c:36)
+}
+
 // ----------------------------------------------------------------- payload hand-off ---
 extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void *stream)
 {

@@ -162,6 +162,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_counters_read": (C.c_int, [vp, vp]),
         "rxg_counters_dev": (vp, [vp]),
         "rxg_rx_replay": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, vp, u32, u32]),
+        "rxg_ether_in": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, C.c_uint16]),
         "rxg_payload_gather_dev": (C.c_int, [vp, C.POINTER(PayloadOut), vp]),
         "rxg_rcv_set": (C.c_int, [vp, i32, u32, u32]),
         "rxg_payload_take": (C.c_int, [vp, i32, u32, u32, C.POINTER(PayloadMsg)]),

@@ -325,6 +325,16 @@ typedef struct rxg_handoff_ops {
 int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
 
+/* Per-packet form with ether_in's contract (etherin.c:12-37: takes ownership of the mbuf,
+   returns 0): a burst of one through the GPU followed by its replay.  For a stack that
+   keeps calling ether_in(m) one mbuf at a time -- its shim is
+     int ether_in(struct rte_mbuf *m) {
+         return rxg_ether_in(g_rxg, &g_ops, m, rte_pktmbuf_mtod(m, void *),
+                             rte_pktmbuf_data_len(m)); }
+   Each call is a GPU round trip; batching (rxg_rx_burst) is the fast path.  Negative on
+   a HIP error (the mbuf is then not consumed). */
+int rxg_ether_in(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *mbuf, void *frame, uint16_t data_len);
+
 /* ------------------------------------------------------------------------- */
 /* Payload hand-off.  The reference copies each       */
 /* in-order segment's payload into a mempool message for the socket ring:     */

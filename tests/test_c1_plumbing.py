@@ -36,3 +36,12 @@ def test_c1_through_rxg(engine, one_burst):
     # every data segment's payload comes from the device gather (in one burst the segments
     # classify to the listener before the replay creates the child, and are gathered anyway)
     assert st.taken == len(MESSAGES)
+
+
+@pytest.mark.gpu
+def test_c1_per_packet_ether_in(engine):
+    """ether_in(m) per mbuf, unchanged call site, each call a GPU burst of one."""
+    st = c1.drive_rxg_per_packet(engine, c1.peer_script(MESSAGES, True))
+    ref = c1.drive_cpu(c1.peer_script(MESSAGES, True))
+    assert st.ring == MESSAGES
+    assert st.log == ref.log and st.rows == ref.rows and st.sent == ref.sent
