@@ -99,6 +99,11 @@ struct RxArgs {
     unsigned long long *counters;
 };
 
+// One frame's record as classify computes it (16 or 48 bytes, rxg.h rxg_rec16/rxg_rec48).
+struct Rec {
+    uint4 q0, q1, q2;
+};
+
 // ------------------------------------------------------------- one round of frames ---
 //
 // Phase A (streaming): the lanes of a group load one frame, sum it and extract its header.
@@ -317,6 +322,257 @@ __device__ __forceinline__ int size_class(uint32_t len)
          : len <= 768u ? 8 : len <= 1024u ? 4 : len <= 1536u ? 5 : len <= 2048u ? 6 : 7;
 }
 
+// Smallest data_len of a class.
+constexpr int class_min_len(int c)
+{
+    return c == 0 ? 0 : c == 1 ? 65 : c == 2 ? 129 : c == 3 ? 257 : c == 8 ? 513 : c == 4 ? 769
+         : c == 5 ? 1025 : c == 6 ? 1537 : 2049;
+}
+
+// ----------------------------------------------------- streaming classes (LPF >= 2) ---
+//
+// The round of the streaming classes is VALU-issue bound, not HBM bound (≈600 VALU per
+// 4 x 1500 B frames in the generic frame_fields, ≈ the whole HBM time at 2.4 GHz), so
+// this path is written for instruction count:
+//  * sums: v_dot2_u32_u16 (acc + lo16 + hi16) is one instruction per dword;
+//  * the fast path masks by data_len only (every lane knows it); the frame's
+//    total_length is needed only when 14 + total_length < data_len, which a wave-uniform
+//    test sends to a slow path that re-sums by the TCP span;
+//  * chunks are masked only where the frame ends: a lane holds at most one partial chunk;
+//  * the leader gathers chunk 1 and 2 (header bytes 16-47) from lanes +1/+2 with DPP
+//    row shifts and the group sum is reduced to it the same way (no LDS traffic);
+//  * loads need no clamp where every frame of the class is long enough (class minimum
+//    length, rounded up to its 64-byte line, which is readable); the others clamp to the
+//    frame's last chunk.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// acc + lo16(x) + hi16(x) (w = 0x00010001) or acc (w = 0)
+__device__ __forceinline__ uint32_t dsum(uint32_t x, uint32_t w, uint32_t acc)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), __builtin_bit_cast(u16x2, w), acc, false);
+}
+constexpr uint32_t kOnes = 0x00010001u;
+
+// lane l <- lane l + K of the same row of 16 lanes (0 past the row's end)
+template <int K>
+__device__ __forceinline__ uint32_t dpp_down(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + K, 0xF, 0xF, false);
+}
+
+// Sum of a group of LPF lanes (aligned at a multiple of LPF), valid in the group's first lane.
+template <int LPF>
+__device__ __forceinline__ uint32_t group_sum(uint32_t t, int lane)
+{
+    if constexpr (LPF >= 2) t += dpp_down<1>(t);
+    if constexpr (LPF >= 4) t += dpp_down<2>(t);
+    if constexpr (LPF >= 8) t += dpp_down<4>(t);
+    if constexpr (LPF >= 16) t += dpp_down<8>(t);
+    if constexpr (LPF >= 64) t += lane_read(t, (lane + 32) & 63);  // rows 0+2, 1+3
+    if constexpr (LPF >= 32) t += lane_read(t, (lane + 16) & 63);
+    return t;
+}
+
+// Adds the chunk's bytes [0, n), n < 16, to the four per-dword accumulators (bytes at or
+// past n read as zero).  Four accumulators: consecutive v_dot2 on one accumulator need a
+// wait state between them.
+__device__ __forceinline__ void partial_sum(const uint32_t (&q)[4], int n, uint32_t (&t)[4])
+{
+    t[0] = dsum(keep_low(q[0], n), kOnes, t[0]);
+    t[1] = dsum(keep_low(q[1], n - 4), kOnes, t[1]);
+    t[2] = dsum(keep_low(q[2], n - 8), kOnes, t[2]);
+    t[3] = dsum(keep_low(q[3], n - 12), kOnes, t[3]);
+}
+
+__device__ __forceinline__ void full_sum(const uint32_t (&q)[4], uint32_t w, uint32_t (&t)[4])
+{
+    t[0] = dsum(q[0], w, t[0]);
+    t[1] = dsum(q[1], w, t[1]);
+    t[2] = dsum(q[2], w, t[2]);
+    t[3] = dsum(q[3], w, t[3]);
+}
+
+// A frame of <= 64 bytes owned by one lane: q = its four chunks, whole chunks at or past
+// data_len already zero.  Same results as frame_fields<1, 4, ...>, fewer instructions.
+template <int MODE>
+__device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32_t (&q)[4][4])
+{
+    constexpr bool TX = MODE == 0;
+    uint32_t h1 = q[0][1], h2 = q[0][2], h3 = q[0][3], h4 = q[1][0], h5 = q[1][1], h6 = q[1][2];
+    uint32_t h7 = q[1][3], h8 = q[2][0], h9 = q[2][1], h10 = q[2][2], h11 = q[2][3];
+    if (__ballot(len < 54u) != 0ull) {  // bytes at/after data_len read as zero (rare)
+        const int L = (int)len;
+        h1 = keep_low(h1, L - 4);   h2 = keep_low(h2, L - 8);   h3 = keep_low(h3, L - 12);
+        h4 = keep_low(h4, L - 16);  h5 = keep_low(h5, L - 20);  h6 = keep_low(h6, L - 24);
+        h7 = keep_low(h7, L - 28);  h8 = keep_low(h8, L - 32);  h9 = keep_low(h9, L - 36);
+        h10 = keep_low(h10, L - 40); h11 = keep_low(h11, L - 44);
+        q[2][0] = h8; q[2][1] = h9; q[2][2] = h10; q[2][3] = h11;
+    }
+    if constexpr (TX) q[3][0] &= 0x0000FFFFu;  // the cksum field (bytes 50-51) is zero while summing
+    const uint32_t tl = bswap16(h4 & 0xFFFFu);
+    const int te = min((int)len, max(34, 14 + (int)tl));  // end of the TCP span
+    const int n2 = te - 32, n3 = te - 48;
+    uint32_t ts[4] = {0u, 0u, 0u, 0u};
+    full_sum(q[2], n2 >= 16 ? kOnes : 0u, ts);
+    full_sum(q[3], n3 >= 16 ? kOnes : 0u, ts);
+    if (n2 > 0 && n2 < 16) partial_sum(q[2], n2, ts);
+    if (n3 > 0 && n3 < 16) partial_sum(q[3], n3, ts);
+    uint32_t tall = dsum(h6 & 0xFFFF0000u, kOnes, ts[0] + ts[1] + ts[2] + ts[3]);
+    tall = dsum(h7, kOnes, tall);
+    tall += 0x0600u + bswap16((tl - 20u) & 0xFFFFu);
+    const uint32_t h6_ip = TX ? (h6 & 0xFFFF0000u) : h6;
+    uint32_t isum = dsum(h3 & 0xFFFF0000u, kOnes, 0u);
+    isum = dsum(h4, kOnes, isum);
+    isum = dsum(h5, kOnes, isum);
+    isum = dsum(h6_ip, kOnes, isum);
+    isum = dsum(h7, kOnes, isum);
+    isum = dsum(h8 & 0xFFFFu, kOnes, isum);
+    const uint32_t ip_ck = (~bswap16(fold16(isum))) & 0xFFFFu;
+    const uint32_t tcp_ck = (~bswap16(fold16(tall))) & 0xFFFFu;
+
+    Fields F;
+    F.ck = ip_ck | (tcp_ck << 16);
+    F.et = bswap16(h3 & 0xFFFFu) | ((h5 >> 24) << 16) | ((h11 >> 24) << 24);
+    F.ports = (bswap16(h9 & 0xFFFFu) << 16) | bswap16(h8 >> 16);
+    F.src = (h6 >> 16) | (h7 << 16);
+    F.dst = (h7 >> 16) | (h8 << 16);
+    F.tl = tl | (((h3 >> 16) & 0xFFu) << 16) | (((h11 >> 16) & 0xFFu) << 24);
+    F.seq = (h9 >> 16) | (h10 << 16);
+    F.ack = (h10 >> 16) | (h11 << 16);
+    F.h1 = h1;
+    F.h2 = h2;
+    if constexpr (TX) {
+        // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118); bytes at or
+        // beyond data_len are never written
+        if (len > 25u) *reinterpret_cast<uint16_t *>(fp + 24) = (uint16_t)bswap16(ip_ck);
+        else if (len > 24u) fp[24] = (uint8_t)(ip_ck >> 8);
+        if (len > 51u) *reinterpret_cast<uint16_t *>(fp + 50) = (uint16_t)bswap16(tcp_ck);
+        else if (len > 50u) fp[50] = (uint8_t)(tcp_ck >> 8);
+    }
+    return F;
+}
+
+template <int C, int LPF, int NLOAD, int MODE, bool NT>
+__device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                                   int lane)
+{
+    static_assert(LPF >= 2 && LPF <= 64, "streaming classes only");
+    constexpr bool TX = MODE == 0;
+    constexpr int SAFE = (class_min_len(C) + 63) & ~63;  // bytes every frame of the class has
+    const int gl = lane & (LPF - 1);
+    const int gbase = lane - gl;
+    const bool leader = active && gl == 0;
+    // inactive lanes: off = len = 0 (the arena's first SAFE bytes exist: it holds a frame of
+    // this class)
+    uint8_t *fp = const_cast<uint8_t *>(a.frames) + (size_t)off * 64u;
+    const uint32_t lastc = len ? ((len - 1u) & ~15u) : 0u;
+
+    uint32_t d[NLOAD][4];
+#pragma unroll
+    for (int j = 0; j < NLOAD; ++j) {
+        const uint32_t o = (uint32_t)(gl + j * LPF) * 16u;
+        uint4 v;
+        if ((j + 1) * LPF * 16 <= SAFE)  // unrolled: constant
+            v = load16<NT>(fp + o);
+        else
+            v = load16<NT>(fp + min(o, lastc));
+        d[j][0] = v.x; d[j][1] = v.y; d[j][2] = v.z; d[j][3] = v.w;
+    }
+
+    // ---- TCP span bytes from 32 on (chunk >= 2), masked at data_len.  Bytes [26, 32) come
+    // from the leader's header dwords below.
+    uint32_t ts[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < NLOAD; ++j) {
+        const int c = gl + j * LPF;
+        const int n = (int)len - c * 16;
+        if (TX && j * LPF <= 3 && 3 < (j + 1) * LPF) {
+            if (c == 3) d[j][0] &= 0x0000FFFFu;  // the cksum field (bytes 50-51) is zero while summing
+        }
+        uint32_t w = n >= 16 ? kOnes : 0u;
+        if (j * LPF < 2) w = c >= 2 ? w : 0u;
+        full_sum(d[j], w, ts);
+        bool part = n > 0 && n < 16;
+        if (j * LPF < 2) part = part && c >= 2;
+        if (part) partial_sum(d[j], n, ts);
+    }
+    uint32_t tsum = ts[0] + ts[1] + ts[2] + ts[3];
+
+    // ---- header dwords 1..11 (bytes 4..47) in the leader: chunk 0 its own, chunk 1 from
+    // lane +1, chunk 2 from lane +2 (LPF 2: the leader's second load)
+    const uint32_t h1 = d[0][1], h2 = d[0][2], h3 = d[0][3];
+    const uint32_t h4 = dpp_down<1>(d[0][0]), h5 = dpp_down<1>(d[0][1]);
+    const uint32_t h6 = dpp_down<1>(d[0][2]), h7 = dpp_down<1>(d[0][3]);
+    uint32_t h8, h9, h10 = 0, h11;
+    if constexpr (LPF == 2) {
+        h8 = d[1][0]; h9 = d[1][1]; h10 = d[1][2]; h11 = d[1][3];
+    } else {
+        h8 = dpp_down<2>(d[0][0]);
+        h9 = dpp_down<2>(d[0][1]);
+        if constexpr (MODE == 48) h10 = dpp_down<2>(d[0][2]);
+        h11 = dpp_down<2>(d[0][3]);
+    }
+    tsum = group_sum<LPF>(tsum, lane);
+
+    const uint32_t tl = bswap16(h4 & 0xFFFFu);  // ip total_length
+    const int E = max(34, 14 + (int)tl);
+    const int tcp_end = min((int)len, E);
+    if (__ballot(leader && tcp_end < (int)len) != 0ull) {
+        // a frame of this round has bytes past its TCP span: re-sum by the span
+        const int te = (int)lane_read((uint32_t)tcp_end, gbase);
+        uint32_t t4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < NLOAD; ++j) {
+            const int c = gl + j * LPF;
+            const int n = te - c * 16;
+            if (c >= 2 && n > 0) {
+                if (n >= 16)
+                    full_sum(d[j], kOnes, t4);
+                else
+                    partial_sum(d[j], n, t4);
+            }
+        }
+        const uint32_t t2 = group_sum<LPF>(t4[0] + t4[1] + t4[2] + t4[3], lane);
+        if (tcp_end < (int)len) tsum = t2;
+    }
+
+    const uint32_t h6_ip = TX ? (h6 & 0xFFFF0000u) : h6;  // TX: hdr_checksum (bytes 24-25) = 0
+    uint32_t isum = dsum(h3 & 0xFFFF0000u, kOnes, 0u);
+    isum = dsum(h4, kOnes, isum);
+    isum = dsum(h5, kOnes, isum);
+    isum = dsum(h6_ip, kOnes, isum);
+    isum = dsum(h7, kOnes, isum);
+    isum = dsum(h8 & 0xFFFFu, kOnes, isum);
+    // pseudo {src, dst (bytes 26..33), 0x00, 0x06, htons(total_length - 20)}: bytes 26..31
+    // here, 32..33 are in chunk 2's lane sum
+    uint32_t tall = dsum(h6 & 0xFFFF0000u, kOnes, tsum);
+    tall = dsum(h7, kOnes, tall);
+    tall += 0x0600u + bswap16((tl - 20u) & 0xFFFFu);
+    const uint32_t ip_ck = (~bswap16(fold16(isum))) & 0xFFFFu;
+    const uint32_t tcp_ck = (~bswap16(fold16(tall))) & 0xFFFFu;
+
+    Fields F;
+    F.ck = ip_ck | (tcp_ck << 16);
+    F.et = bswap16(h3 & 0xFFFFu) | ((h5 >> 24) << 16) | ((h11 >> 24) << 24);
+    F.ports = (bswap16(h9 & 0xFFFFu) << 16) | bswap16(h8 >> 16);
+    F.src = (h6 >> 16) | (h7 << 16);
+    F.dst = (h7 >> 16) | (h8 << 16);
+    F.tl = tl | (((h3 >> 16) & 0xFFu) << 16) | (((h11 >> 16) & 0xFFu) << 24);
+    F.seq = (h9 >> 16) | (h10 << 16);
+    F.ack = (h10 >> 16) | (h11 << 16);
+    F.h1 = h1;
+    F.h2 = h2;
+    if constexpr (TX) {
+        // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118); frames of
+        // these classes are longer than 64 bytes
+        if (leader) {
+            *reinterpret_cast<uint16_t *>(fp + 24) = (uint16_t)bswap16(ip_ck);
+            *reinterpret_cast<uint16_t *>(fp + 50) = (uint16_t)bswap16(tcp_ck);
+        }
+    }
+    return F;
+}
+
 template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
                                           int lane_in, uint32_t *sf)
@@ -354,7 +610,15 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
         }
         int rl = lane;
         asm volatile("" : "+v"(rl));  // keep per-round lane math inside the round (VGPRs)
-        const Fields F = frame_round<LPF, NLOAD, JUMBO, MODE, NT>(a, koff, act ? klen : 0u, act, rl);
+        Fields F;
+        if constexpr (LPF == 1) {
+            uint32_t d[4][4];
+            load_chunks<1, 4, NT>(a, koff, act ? klen : 0u, act, rl, d);
+            F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
+        } else if constexpr (LPF >= 2 && !JUMBO)
+            F = frame_round_fast<C, LPF, NLOAD, MODE, NT>(a, act ? koff : 0u, act ? klen : 0u, act, rl);
+        else
+            F = frame_round<LPF, NLOAD, JUMBO, MODE, NT>(a, koff, act ? klen : 0u, act, rl);
         if constexpr (MODE != 0) {
             if (act && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, korig, F);
         }
@@ -363,7 +627,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
 
 // Phase B: lane i classifies frame i of the slice (all 64 probes in flight together) and
 // writes its record; the records of a slice are one contiguous 1 KiB / 3 KiB store.
-// STRIP (experiment builds only): 1 = no frame loads, 2 = no TCB probe, 4 = no record store
+// STRIP (experiment builds only): 2 = no TCB probe, 4 = no record store, 8 = no phase B
 // First bucket of the exact-tuple probe, loaded early so that several frames' probes of
 // one lane are in flight together.
 struct Probe {
@@ -384,21 +648,32 @@ __device__ __forceinline__ Probe probe_issue(const RxArgs &a, bool valid, const 
     return P;
 }
 
-template <int MODE, int STRIP = 0>
-__device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
-                                                const Fields &F, const Probe &P, WaveCounters &wc);
+__device__ __forceinline__ Probe probe_none()
+{
+    Probe P;
+    P.s0 = P.s1 = P.s2 = P.s3 = make_uint4(0u, 0u, 0u, kEmpty);
+    P.hb = 0;
+    return P;
+}
 
 template <int MODE, int STRIP = 0>
+__device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
+                                                const Fields &F, const Probe &P, WaveCounters &wc,
+                                                Rec &pr);
+
+// Classify lane's frame and leave its record in pr (the caller stores it, now or deferred).
+template <int MODE, int STRIP = 0>
 __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
-                                               const Fields &F, WaveCounters &wc)
+                                               const Fields &F, WaveCounters &wc, Rec &pr)
 {
-    const Probe P = probe_issue(a, valid && !(STRIP & 2), F);
-    classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc);
+    const Probe P = (STRIP & 2) ? probe_none() : probe_issue(a, valid, F);
+    classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr);
 }
 
 template <int MODE, int STRIP>
 __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
-                                                const Fields &F, const Probe &P, WaveCounters &wc)
+                                                const Fields &F, const Probe &P, WaveCounters &wc,
+                                                Rec &pr)
 {
     const uint32_t ck = valid ? F.ck : 0u, w_et = valid ? F.et : 0u, ports = valid ? F.ports : 0u;
     const uint32_t src_raw = valid ? F.src : 0u, dst_raw = valid ? F.dst : 0u, w_tl = valid ? F.tl : 0u;
@@ -479,14 +754,14 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
                            (trunc ? RXG_F_TRUNC : 0u) | (arp_learn ? RXG_F_ARP_LEARN : 0u);
     const int32_t datalen = (int32_t)tl - (int32_t)(vihl & 0xFu) * 4 - (int32_t)(doff >> 4) * 4;
 
-    if (valid && !(STRIP & 4)) {
+    (void)f;
+    {
         uint4 q0;
         q0.x = (uint32_t)idx;
         q0.y = ipc | (tcc << 16);
         q0.z = verdict | (st << 8) | (tflags << 16) | (flags << 24);
         q0.w = (uint32_t)datalen;
-        uint4 *rec = reinterpret_cast<uint4 *>(a.out + (size_t)f * MODE);
-        rec[0] = q0;
+        pr.q0 = q0;
         if constexpr (MODE == 48) {
             const uint32_t seq_raw = F.seq, ack_raw = F.ack, h1 = F.h1, h2 = F.h2;
             uint4 q1, q2;
@@ -498,8 +773,8 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
             q2.y = dst_raw;
             q2.z = doff | ((h1 >> 16) << 8) | ((h2 & 0xFFu) << 24);
             q2.w = h2 >> 8;
-            rec[1] = q1;
-            rec[2] = q2;
+            pr.q1 = q1;
+            pr.q2 = q2;
         }
     }
 
@@ -571,7 +846,51 @@ __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane,
     len = ok ? l : 0u;
 }
 
-template <int MODE, int CMASK, bool NT, bool PAIR = false, int STRIP = 0, bool SEL = false>
+// Records of a wave's slices are staged in LDS and written out RS slices at a time (and
+// at the end): record stores interleaved with the frame stream cost ≈10 % of the C3 kernel
+// (measured: 271 µs with 1 KiB stored per slice as it completes, 244 µs staged and
+// written at the end, 243 µs with no record stores at all), HBM read/write turnarounds.
+template <int MODE, int RS>
+struct RecRing {
+    static constexpr int kQ = MODE / 16;  // uint4 per record
+    uint4 (*img)[kQ * 64];                // [RS][kQ * 64]: the slice's records, contiguous
+    uint32_t *base;                       // [RS]: first frame of the slot's slice
+    uint32_t n = 0;                       // slots in use (wave-uniform)
+
+    __device__ __forceinline__ void put(uint32_t slice, int lane, const Rec &r)
+    {
+        uint4 *q = img[n] + lane * kQ;
+        q[0] = r.q0;
+        if constexpr (kQ == 3) {
+            q[1] = r.q1;
+            q[2] = r.q2;
+        }
+        if (lane == 0) base[n] = slice * 64u;
+        ++n;
+    }
+
+    // Writes out every staged slice: uint4 k*64 + lane of each slot, so a wave-instruction
+    // stores 1 KiB contiguously.  Records of frames >= n_frames are not written.
+    __device__ __forceinline__ void flush(const RxArgs &a, int lane)
+    {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)base[i]);
+            uint4 *dst = reinterpret_cast<uint4 *>(a.out + (size_t)f0 * MODE);
+#pragma unroll
+            for (int k = 0; k < kQ; ++k) {
+                const int idx = k * 64 + lane;
+                if (f0 + (uint32_t)(idx / kQ) < a.n) dst[idx] = img[i][idx];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // slots are rewritten after every lane's read
+        n = 0;
+    }
+};
+
+template <int MODE, int CMASK, bool NT, bool PAIR = false, int STRIP = 0, bool SEL = false, int RS16 = 8>
 __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 {
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -580,6 +899,12 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     constexpr int kWaveLds = MODE == 0 ? 1 : (NF * 64 > 1024 ? NF * 64 : 1024);
     __shared__ __attribute__((aligned(16))) uint32_t s_fields[4][kWaveLds];
     __shared__ unsigned long long s_cnt[4][RXG_NCOUNTERS];
+    // record ring: REC16 8 slices (8 KiB) per wave, REC48 4 (12 KiB); LDS-limited to 3 / 2
+    // workgroups per CU (measured best of 2 / 3 / 4 over C2, C3, C4: DESIGN.md §5)
+    constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : 1;
+    constexpr int kQ = MODE == 0 ? 1 : MODE / 16;
+    __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kQ * 64];
+    __shared__ uint32_t s_recf[4][RS];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
@@ -591,6 +916,10 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 #pragma unroll
     for (int k = 0; k < RXG_NCOUNTERS; ++k) wc.c[k] = 0u;
     unsigned long long bytes = 0ull;
+    RecRing<MODE == 0 ? 16 : MODE, RS> ring;
+    ring.img = s_rec[wid];
+    ring.base = s_recf[wid];
+    Rec rec;
 
     // Descriptors: (c_off, c_len) for slice s, (n_off, n_len) for slice s + nwaves, whose
     // loads are always in flight while slice s is processed.
@@ -620,17 +949,21 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
                 load_desc<SEL>(a, s + (pair ? 3u : 2u) * nwaves, lane, y_off, y_len);
                 uint32_t dA[4][4], dB[4][4];
                 transpose_small_slice(vA, lane, sf, dA);
-                const Fields FA = frame_fields<1, 4, false, MODE, false>(a, c_off, c_len, true, lane, dA);
+                const Fields FA = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)c_off * 64u, c_len, dA);
                 Fields FB = FA;
                 if (pair) {
                     transpose_small_slice(vB, lane, sf, dB);
-                    FB = frame_fields<1, 4, false, MODE, false>(a, n_off, n_len, true, lane, dB);
+                    FB = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)n_off * 64u, n_len, dB);
                 }
-                classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, FA, wc);
+                classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, FA, wc, rec);
                 bytes += c_len;
+                if (ring.n == RS) ring.flush(a, lane);
+                ring.put(s, lane, rec);
                 if (pair) {
-                    classify_store<MODE, STRIP>(a, s2 * 64u + (uint32_t)lane, true, n_len, FB, wc);
+                    classify_store<MODE, STRIP>(a, s2 * 64u + (uint32_t)lane, true, n_len, FB, wc, rec);
                     bytes += n_len;
+                    if (ring.n == RS) ring.flush(a, lane);
+                    ring.put(s2, lane, rec);
                 }
                 s += (pair ? 2u : 1u) * nwaves;
                 c_off = x_off; c_len = x_len;
@@ -648,20 +981,25 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 7) & 1) run_class<7, 64, 2, true, MODE, NT>(a, cls, off, len, lane, sf);
-        if constexpr (MODE == 0) {
+        if constexpr (MODE == 0 || (STRIP & 8)) {
             wcount(wc, RXG_C_RX, valid);
         } else {
             // the fields parked by other lanes of this wave must be visible to this lane
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            classify_store<MODE>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc);
+            classify_store<MODE, STRIP>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc, rec);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
+            if (!(STRIP & 4)) {
+                if (ring.n == RS) ring.flush(a, lane);
+                ring.put(s, lane, rec);
+            }
         }
         s += nwaves;
         c_off = n_off; c_len = n_len;
         load_desc<SEL>(a, s + nwaves, lane, n_off, n_len);
     }
+    if constexpr (MODE != 0) ring.flush(a, lane);
 
     if (a.counters == nullptr) return;
     // wave -> workgroup -> one atomic per counter
@@ -829,6 +1167,12 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 5: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 6: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
         case 7: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 2>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 9: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 4>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 10: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 8>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 11: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 6>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 12: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, false, 15>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 13: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, false, 5>), dim3(blocks), dim3(256), 0, st, a); break;
         default: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
     } else if (L.mode == 48) {

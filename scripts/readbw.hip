@@ -1,0 +1,136 @@
+// readbw.hip — read-bandwidth ceilings for the rx kernel's access pattern (experiment tool,
+// not part of librxg).  Build: hipcc --offload-arch=gfx950 -O3 -o build/readbw scripts/readbw.hip
+//
+// Variants (all read a buffer far larger than the 256 MiB Infinity Cache, sum every dword,
+// one store per thread at the end):
+//   flat_def / flat_nt   grid-stride 16 B per lane, U loads in flight per lane
+//   fr1536 / fr1504      1500-byte frames in 1536-B (64-B aligned) or 1504-B (16-B aligned)
+//                        slots, 16 lanes per frame x 6 loads: the rx kernel's C3 class
+//                        without its compute
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void flat(const u32x4 *buf, size_t n16, unsigned *out)
+{
+    const size_t stride = (size_t)gridDim.x * 256u;
+    size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+    unsigned acc = 0;
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld<NT>(buf + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    for (; i < n16; i += stride) {
+        u32x4 v = ld<NT>(buf + i);
+        acc += v.x + v.y + v.z + v.w;
+    }
+    out[blockIdx.x * 256u + threadIdx.x] = acc;
+}
+
+// frames: slot bytes SLOT, 1500 bytes each; a wave takes 4 frames per round (16 lanes each),
+// waves own slices of 64 consecutive frames (like rx_kernel)
+template <bool NT, int SLOT>
+__global__ __launch_bounds__(256) void frames(const uint8_t *buf, unsigned nfr, unsigned *out)
+{
+    const int lane = threadIdx.x & 63;
+    const unsigned wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const unsigned nwaves = gridDim.x * 4u;
+    const unsigned nsl = (nfr + 63u) / 64u;
+    unsigned acc = 0;
+    const int gl = lane & 15;
+    for (unsigned s = wave; s < nsl; s += nwaves) {
+        for (unsigned r = 0; r < 64; r += 4) {
+            const unsigned f = s * 64u + r + (unsigned)(lane >> 4);
+            if (f >= nfr) break;
+            const uint8_t *fp = buf + (size_t)f * SLOT;
+            u32x4 v[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int c = gl + 16 * j;
+                const bool ok = c * 16 < 1500;
+                v[j] = ld<NT>(reinterpret_cast<const u32x4 *>(fp + (ok ? c * 16 : 0)));
+                if (!ok) v[j] = u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) acc += v[j].x + v[j].y + v[j].z + v[j].w;
+        }
+    }
+    out[blockIdx.x * 256u + threadIdx.x] = acc;
+}
+
+template <typename F>
+static void timeit(const char *name, double bytes, F launch)
+{
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) launch();
+    std::vector<float> ms;
+    for (int i = 0; i < 20; ++i) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float t;
+        CK(hipEventElapsedTime(&t, a, b));
+        ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    const double med = ms[ms.size() / 2];
+    printf("{\"variant\": \"%s\", \"us_median\": %.2f, \"us_min\": %.2f, \"TBps\": %.3f}\n", name, med * 1e3,
+           ms[0] * 1e3, bytes / (med * 1e-3) / 1e12);
+    fflush(stdout);
+}
+
+int main()
+{
+    const unsigned nfr = 1u << 20;
+    const size_t bytes = (size_t)nfr * 1536u;  // 1.61 GB
+    uint8_t *buf;
+    unsigned *out;
+    CK(hipMalloc(&buf, bytes + 4096));
+    CK(hipMemset(buf, 1, bytes + 4096));
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    const int maxg = ncu * 32;
+    CK(hipMalloc(&out, (size_t)maxg * 256 * sizeof(unsigned)));
+    const size_t n16_a = (size_t)nfr * 1500u / 16u;  // the algorithmic byte count of C3
+    for (int rep = 0; rep < 2; ++rep) {
+        for (int g : {ncu * 4, ncu * 8, ncu * 16}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "flat_def_u4_g%d", g);
+            timeit(nm, n16_a * 16.0, [&] { flat<false, 4><<<g, 256>>>((const u32x4 *)buf, n16_a, out); });
+            snprintf(nm, sizeof nm, "flat_nt_u4_g%d", g);
+            timeit(nm, n16_a * 16.0, [&] { flat<true, 4><<<g, 256>>>((const u32x4 *)buf, n16_a, out); });
+            snprintf(nm, sizeof nm, "flat_nt_u8_g%d", g);
+            timeit(nm, n16_a * 16.0, [&] { flat<true, 8><<<g, 256>>>((const u32x4 *)buf, n16_a, out); });
+            snprintf(nm, sizeof nm, "fr1536_nt_g%d", g);
+            timeit(nm, nfr * 1500.0, [&] { frames<true, 1536><<<g, 256>>>(buf, nfr, out); });
+            snprintf(nm, sizeof nm, "fr1536_def_g%d", g);
+            timeit(nm, nfr * 1500.0, [&] { frames<false, 1536><<<g, 256>>>(buf, nfr, out); });
+            snprintf(nm, sizeof nm, "fr1504_nt_g%d", g);
+            timeit(nm, nfr * 1500.0, [&] { frames<true, 1504><<<g, 256>>>(buf, nfr, out); });
+        }
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
