@@ -20,6 +20,8 @@
 //   * Counters: wave-uniform ballot counts, one u64 atomic per counter per workgroup.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rxg_common.h"
 #include "rxg_kernels.h"
 
@@ -392,8 +394,9 @@ __device__ __forceinline__ void full_sum(const uint32_t (&q)[4], uint32_t w, uin
     t[3] = dsum(q[3], w, t[3]);
 }
 
-// A frame of <= 64 bytes owned by one lane: q = its four chunks, whole chunks at or past
-// data_len already zero.  Same results as frame_fields<1, 4, ...>, fewer instructions.
+// A frame of <= 64 bytes owned by one lane: q = its four chunks as loaded (bytes at or past
+// data_len may hold anything: every use below masks them).  Same results as
+// frame_fields<1, 4, ...>, fewer instructions.
 template <int MODE>
 __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32_t (&q)[4][4])
 {
@@ -648,6 +651,17 @@ __device__ __forceinline__ Probe probe_issue(const RxArgs &a, bool valid, const 
     return P;
 }
 
+// Per-lane last-flow cache: the findtcb result of the last TCP frame this lane classified
+// (the table does not change during a launch).  A slice whose TCP frames all hit their
+// lane's cache skips the probe, the findtcb loop and the ARP-mirror probe: a burst of
+// one flow (C2, bulk-transfer trains) classifies without a dependent L2 round trip.
+struct FlowCache {
+    uint32_t ports = 0, dst = 0, src = 0;  // tuple as pass 1 compares it
+    int32_t idx = -1;
+    uint32_t meta = 0;                     // st | lhit << 8 | nslot << 9 | arp_learn << 10 | valid << 31
+};
+constexpr uint32_t kFcValid = 0x80000000u;
+
 __device__ __forceinline__ Probe probe_none()
 {
     Probe P;
@@ -659,21 +673,29 @@ __device__ __forceinline__ Probe probe_none()
 template <int MODE, int STRIP = 0>
 __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
                                                 const Fields &F, const Probe &P, WaveCounters &wc,
-                                                Rec &pr);
+                                                Rec &pr, FlowCache &fc, bool cached);
 
-// Classify lane's frame and leave its record in pr (the caller stores it, now or deferred).
+__device__ __forceinline__ bool fc_hit(const FlowCache &fc, const Fields &F)
+{
+    return (fc.meta & kFcValid) && fc.ports == F.ports && fc.dst == F.dst && fc.src == bswap32(F.src);
+}
+
+// Classify lane's frame and leave its record in pr.
 template <int MODE, int STRIP = 0>
 __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
-                                               const Fields &F, WaveCounters &wc, Rec &pr)
+                                               const Fields &F, WaveCounters &wc, Rec &pr, FlowCache &fc)
 {
-    const Probe P = (STRIP & 2) ? probe_none() : probe_issue(a, valid, F);
-    classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr);
+    const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
+    const bool is_tcp = valid && et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
+    const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
+    const Probe P = ((STRIP & 2) || cached) ? probe_none() : probe_issue(a, valid, F);
+    classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr, fc, cached);
 }
 
 template <int MODE, int STRIP>
 __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
                                                 const Fields &F, const Probe &P, WaveCounters &wc,
-                                                Rec &pr)
+                                                Rec &pr, FlowCache &fc, bool cached)
 {
     const uint32_t ck = valid ? F.ck : 0u, w_et = valid ? F.et : 0u, ports = valid ? F.ports : 0u;
     const uint32_t src_raw = valid ? F.src : 0u, dst_raw = valid ? F.dst : 0u, w_tl = valid ? F.tl : 0u;
@@ -686,7 +708,7 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
     const bool trunc = valid && len < 54u;
     // ip.c:30-32: would get_mac(ntohl(src)) fail?  (ARP mirror enabled only)
     bool arp_learn = false;
-    if (is_tcp && a.t.arp != nullptr) {
+    if (is_tcp && a.t.arp != nullptr && !cached) {
         const uint32_t ip = bswap32(src_raw);
         uint32_t h = arp_hash(ip) & a.t.arp_mask;
         arp_learn = true;
@@ -703,7 +725,15 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
     int32_t idx = -1;
     bool lhit = false, nslot = false;
     uint32_t st = RXG_STATE_NONE;
-    if (is_tcp && !(STRIP & 2)) {
+    if (cached) {  // every TCP lane of the wave hits its cache (wave-uniform)
+        if (is_tcp) {
+            idx = fc.idx;
+            st = fc.meta & 0xFFu;
+            lhit = (fc.meta >> 8) & 1u;
+            nslot = (fc.meta >> 9) & 1u;
+            arp_learn = (fc.meta >> 10) & 1u;
+        }
+    } else if (is_tcp && !(STRIP & 2)) {
         uint32_t hb = P.hb;
         uint4 s0 = P.s0, s1 = P.s1, s2 = P.s2, s3 = P.s3;
         for (uint32_t probe = 0; probe <= a.t.bucket_mask; ++probe) {
@@ -731,6 +761,11 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
             nslot = a.t.min_null < (L >= 0 ? L : a.t.ntcb);
             if (lhit) st = RXG_LISTENING;
         }
+        fc.ports = ports;
+        fc.dst = dst_raw;
+        fc.src = src_host;
+        fc.idx = idx;
+        fc.meta = st | ((uint32_t)lhit << 8) | ((uint32_t)nslot << 9) | ((uint32_t)arp_learn << 10) | kFcValid;
     }
 
     // ---- verdict (etherin.c:21-35, ip.c:28-39, tcp_in.c:47-72)
@@ -778,7 +813,20 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
         }
     }
 
-    // ---- counters (definition: oracle orc_count_record)
+    // ---- counters (definition: oracle orc_count_record).  Common case first: every valid
+    // frame of the wave is a TCP segment with good checksums dispatched to an exact-match
+    // TCB; then five counters move by the same count and the other ten not at all.
+    const bool plain = is_tcp && verdict == RXG_V_DISPATCH && !lhit && !nslot && !trunc && ipc == 0u &&
+                       tcc == 0u;
+    if (__ballot(valid && !plain) == 0ull) {
+        const uint32_t nv = (uint32_t)__popcll(__ballot(valid));
+        wc.c[RXG_C_RX] += nv;
+        wc.c[RXG_C_IPV4] += nv;
+        wc.c[RXG_C_TCP] += nv;
+        wc.c[RXG_C_TCB_HIT_EXACT] += nv;
+        wc.c[RXG_C_DISPATCH] += nv;
+        return;
+    }
     wcount(wc, RXG_C_RX, valid);
     wcount(wc, RXG_C_TRUNC, trunc);
     wcount(wc, RXG_C_IPV4, is_ip);
@@ -808,25 +856,33 @@ __device__ __forceinline__ void issue_small_slice(const RxArgs &a, uint32_t off,
         const int fr = 16 * j + (lane >> 2);
         const uint32_t foff = lane_read(off, fr), flen = lane_read(len, fr);
         const bool ok = (uint32_t)(ch * 16) < flen;  // frames <= 64 B: a whole 64-B slot
-        const uint4 q = load16<NT>(ok ? a.frames + (size_t)foff * 64u + ch * 16 : a.frames);
-        v[j] = ok ? q : make_uint4(0u, 0u, 0u, 0u);
+        // chunks past data_len read the arena's first bytes and are left as loaded
+        // (fields_small masks every byte at or past data_len); no select on the result, so
+        // nothing waits for the load here
+        v[j] = load16<NT>(ok ? a.frames + (size_t)foff * 64u + ch * 16 : a.frames);
     }
 }
 
-// ... writes it to the wave's LDS at [frame][chunk], and after a wave barrier lane i reads
-// back frame i's 64 bytes.
+// ... writes it to the wave's LDS at [frame][chunk ^ ((frame >> 2) & 3)], and after a wave
+// barrier lane i reads back frame i's 64 bytes.  The XOR swizzle makes the 16 lanes of a
+// ds_read_b128 group read 16 different 16-byte bank columns (unswizzled, lanes 4 frames
+// apart collide: 4-way conflicts, ≈48 LDS cycles per slice measured).
 __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int lane, uint32_t *sf,
                                                       uint32_t (&d)[4][4])
 {
     uint4 *t = reinterpret_cast<uint4 *>(sf);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) t[j * 64 + lane] = v[j];  // [frame 16j + l/4][chunk l&3]
+    for (int j = 0; j < 4; ++j) {
+        const int fr = 16 * j + (lane >> 2), ch = lane & 3;
+        t[fr * 4 + (ch ^ ((fr >> 2) & 3))] = v[j];
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int sw = (lane >> 2) & 3;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const uint4 q = t[lane * 4 + c];
+        const uint4 q = t[lane * 4 + (c ^ sw)];
         d[c][0] = q.x; d[c][1] = q.y; d[c][2] = q.z; d[c][3] = q.w;
     }
     __builtin_amdgcn_wave_barrier();  // reads done before the LDS is reused
@@ -835,15 +891,15 @@ __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int l
 template <bool SEL>
 __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane, uint32_t &off, uint32_t &len)
 {
-    // unconditional (clamped) loads, invalid lanes zeroed afterwards: see load_chunks
+    // Unconditional loads of a clamped index (a.n >= 1), not masked here: masking would
+    // consume the load at once, and s_waitcnt retires in order, so the wait would also
+    // drain every older load in flight (the prefetched frames of the small-slice
+    // pipeline).  Callers treat lanes with frame index >= a.n as invalid.
     const uint32_t f = s * 64u + (uint32_t)lane;
-    const bool ok = s < ((a.n + 63u) >> 6) && f < a.n;
-    const uint32_t fc = ok ? f : 0u;
+    const uint32_t fc = min(f, a.n - 1u);
     const uint32_t pf = SEL ? a.sel[fc] : fc;
-    const uint32_t o = a.off64[pf];
-    const uint32_t l = a.len[pf];
-    off = ok ? o : 0u;
-    len = ok ? l : 0u;
+    off = a.off64[pf];
+    len = a.len[pf];
 }
 
 // Records of a wave's slices are staged in LDS and written out RS slices at a time (and
@@ -856,6 +912,17 @@ struct RecRing {
     uint4 (*img)[kQ * 64];                // [RS][kQ * 64]: the slice's records, contiguous
     uint32_t *base;                       // [RS]: first frame of the slot's slice
     uint32_t n = 0;                       // slots in use (wave-uniform)
+
+    // LDS scratch of `bytes` in the free slots (the small-slice transpose, the parked
+    // fields of the class path): the slots after the used ones, flushing first if fewer
+    // are free.  The slice's own record later goes to the first of them (put), after the
+    // scratch has been read.
+    __device__ __forceinline__ uint32_t *scratch(const RxArgs &a, int lane, int bytes)
+    {
+        const uint32_t need = (uint32_t)((bytes + kQ * 1024 - 1) / (kQ * 1024));
+        if (n + need > (uint32_t)RS) flush(a, lane);
+        return reinterpret_cast<uint32_t *>(img[n]);
+    }
 
     __device__ __forceinline__ void put(uint32_t slice, int lane, const Rec &r)
     {
@@ -890,19 +957,47 @@ struct RecRing {
     }
 };
 
-template <int MODE, int CMASK, bool NT, bool PAIR = false, int STRIP = 0, bool SEL = false, int RS16 = 8>
+// One all-small slice s whose frames are in flight in vb[P]; prefetches slice s + nwaves
+// into vb[1-P] when it is all-small too (and returns true: the caller continues the run).
+template <int P, int MODE, int STRIP, bool SEL, int RS>
+__device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &s, uint32_t nslices,
+                                           uint32_t nwaves, uint32_t &c_off, uint32_t &c_len, uint32_t &n_off,
+                                           uint32_t &n_len, uint4 (&vb)[2][4], RecRing<MODE, RS> &ring,
+                                           WaveCounters &wc, Rec &rec, FlowCache &fc, unsigned long long &bytes)
+{
+    uint32_t y_off, y_len;
+    load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len);
+    const uint32_t s1 = s + nwaves;
+    const bool nxt = s1 < nslices && s1 * 64u + 64u <= a.n && __ballot(n_len <= 64u) == ~0ull;
+    if (nxt) issue_small_slice<false>(a, n_off, n_len, lane, vb[1 - P]);
+    uint32_t d[4][4];
+    uint32_t *sf = ring.scratch(a, lane, 4096);
+    transpose_small_slice(vb[P], lane, sf, d);
+    const Fields F = fields_small<MODE>(nullptr, c_len, d);
+    classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, wc, rec, fc);
+    bytes += c_len;
+    if (!(STRIP & 4)) {
+        if (ring.n == RS) ring.flush(a, lane);
+        ring.put(s, lane, rec);
+    }
+    s = s1;
+    c_off = n_off; c_len = n_len;
+    n_off = y_off; n_len = y_len;
+    return nxt;
+}
+
+template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11>
 __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 {
     constexpr int NF = MODE == 48 ? NF48 : NF16;
-    // per-wave LDS: the parked fields of the general path, or the 4 KiB transpose of an
-    // all-small slice (never both at once)
-    constexpr int kWaveLds = MODE == 0 ? 1 : (NF * 64 > 1024 ? NF * 64 : 1024);
-    __shared__ __attribute__((aligned(16))) uint32_t s_fields[4][kWaveLds];
     __shared__ unsigned long long s_cnt[4][RXG_NCOUNTERS];
-    // record ring: REC16 8 slices (8 KiB) per wave, REC48 4 (12 KiB); LDS-limited to 3 / 2
-    // workgroups per CU (measured best of 2 / 3 / 4 over C2, C3, C4: DESIGN.md §5)
+    // Per-wave LDS = the record ring (REC16: RS16 = 11 slices of 1 KiB, REC48: 4 of 3 KiB,
+    // 3 workgroups per CU: the best of 2-5 per CU over C2, C3, C4); its
+    // free slots are also the scratch of the slice in progress (4 KiB small-slice transpose,
+    // NF x 256 B parked fields), so LDS per wave is the ring alone and sets the occupancy.
     constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : 1;
     constexpr int kQ = MODE == 0 ? 1 : MODE / 16;
+    static_assert(MODE == 0 || RS * kQ * 1024 >= 4096 + kQ * 1024, "ring too small for the scratch");
     __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kQ * 64];
     __shared__ uint32_t s_recf[4][RS];
     const int lane = threadIdx.x & 63;
@@ -910,7 +1005,6 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
     const uint32_t nwaves = gridDim.x * 4u;
     const uint32_t nslices = (a.n + 63u) >> 6;
-    uint32_t *sf = s_fields[wid];
 
     WaveCounters wc;
 #pragma unroll
@@ -920,6 +1014,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     ring.img = s_rec[wid];
     ring.base = s_recf[wid];
     Rec rec;
+    FlowCache fcache;
 
     // Descriptors: (c_off, c_len) for slice s, (n_off, n_len) for slice s + nwaves, whose
     // loads are always in flight while slice s is processed.
@@ -934,44 +1029,28 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         const int cls = valid ? size_class(len) : 9;
         if constexpr (MODE != 0 && (CMASK & 1)) {
             if (__ballot(cls == 0) == ~0ull) {
-                // All-small slices: every frame <= 64 bytes; lane i owns frame i end to end
-                // (fields stay in registers).  Two such slices (s and s + nwaves) are done
-                // together when both are all-small: both slices' loads, then both probes,
-                // are in flight at once (one latency chain for two slices).
-                const uint32_t s2 = s + nwaves;
-                const bool pair = PAIR && __ballot(s2 < nslices && s2 * 64u + (uint32_t)lane < a.n &&
-                                                   n_len <= 64u) == ~0ull;
-                uint4 vA[4], vB[4];
-                issue_small_slice<false>(a, c_off, c_len, lane, vA);
-                if (pair) issue_small_slice<false>(a, n_off, n_len, lane, vB);
-                uint32_t x_off = n_off, x_len = n_len, y_off = 0, y_len = 0;
-                if (pair) load_desc<SEL>(a, s + 2u * nwaves, lane, x_off, x_len);
-                load_desc<SEL>(a, s + (pair ? 3u : 2u) * nwaves, lane, y_off, y_len);
-                uint32_t dA[4][4], dB[4][4];
-                transpose_small_slice(vA, lane, sf, dA);
-                const Fields FA = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)c_off * 64u, c_len, dA);
-                Fields FB = FA;
-                if (pair) {
-                    transpose_small_slice(vB, lane, sf, dB);
-                    FB = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)n_off * 64u, n_len, dB);
+                // A run of all-small slices (every frame <= 64 bytes; lane i owns frame i end
+                // to end), prefetched one slice deep: the next slice's frame loads are issued
+                // before this slice's are waited for.  vmcnt retires in order, so the loads
+                // are issued youngest-last (descriptors two slices ahead, then the next
+                // slice's frames) and every wait leaves the next slice's frames in flight.
+                // The two frame buffers alternate between the unrolled steps P = 0, 1 (a
+                // register copy of a load in flight would wait for it).
+                uint4 vb[2][4];
+                issue_small_slice<false>(a, c_off, c_len, lane, vb[0]);
+                for (;;) {
+                    if (!small_step<0, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
+                                                             n_len, vb, ring, wc, rec, fcache, bytes))
+                        break;
+                    if (!small_step<1, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
+                                                             n_len, vb, ring, wc, rec, fcache, bytes))
+                        break;
                 }
-                classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, FA, wc, rec);
-                bytes += c_len;
-                if (ring.n == RS) ring.flush(a, lane);
-                ring.put(s, lane, rec);
-                if (pair) {
-                    classify_store<MODE, STRIP>(a, s2 * 64u + (uint32_t)lane, true, n_len, FB, wc, rec);
-                    bytes += n_len;
-                    if (ring.n == RS) ring.flush(a, lane);
-                    ring.put(s2, lane, rec);
-                }
-                s += (pair ? 2u : 1u) * nwaves;
-                c_off = x_off; c_len = x_len;
-                n_off = y_off; n_len = y_len;
                 continue;
             }
         }
         bytes += len;
+        uint32_t *sf = MODE == 0 ? nullptr : ring.scratch(a, lane, NF * 256);
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
@@ -988,7 +1067,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            classify_store<MODE, STRIP>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc, rec);
+            classify_store<MODE, STRIP>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc, rec, fcache);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
             if (!(STRIP & 4)) {
                 if (ring.n == RS) ring.flush(a, lane);
@@ -1155,7 +1234,7 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     // production kernels use non-temporal loads for the >256 B classes (measured +5 %
     // at 1500 B, -4 % at 64 B: classes 0-2 always use plain loads)
     if (L.sel) {  // re-classification of selected frames (rxg_rx_replay), records of 16 B
-        hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, true>), dim3(blocks), dim3(256), 0, st, a);
         return hipGetLastError();
     }
     if (L.mode == 16) {
@@ -1163,16 +1242,20 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 1: hipLaunchKernelGGL((rx_kernel<16, 0x01, false>), dim3(blocks), dim3(256), 0, st, a); break;
         case 2: hipLaunchKernelGGL((rx_kernel<16, 0x20, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 3: hipLaunchKernelGGL((rx_kernel<16, 0xFF, false>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 4: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, true>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 5: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 6: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 7: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 8: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 2>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 9: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 4>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 10: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 8>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 11: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, false, 6>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 12: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, false, 15>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 13: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, false, 0, false, 5>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 9: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 10: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 8>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 11: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 6>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 12: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 15>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 13: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 5>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 14: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 6>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 15: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 20: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 0, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 21: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 2, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 22: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 4, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 23: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 6, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 24: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 128, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 25: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 134, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
         default: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
     } else if (L.mode == 48) {
