@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -77,6 +78,38 @@ __global__ __launch_bounds__(256) void frames(const uint8_t *buf, unsigned nfr, 
     out[blockIdx.x * 256u + threadIdx.x] = acc;
 }
 
+// C2 pattern: 64-byte frames, slices of 64 frames per wave (round-robin), descriptors
+// off64[] (u32) and len[] (u16) read per slice; MODE bit 0: read descriptors (else
+// frame f at slot f), bit 1: store a 16-byte record per frame (1 KiB per slice).
+template <int MODE>
+__global__ __launch_bounds__(256) void small(const uint8_t *buf, const unsigned *off64, const unsigned short *len,
+                                             unsigned nfr, uint4 *rec, unsigned *out)
+{
+    const int lane = threadIdx.x & 63;
+    const unsigned wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const unsigned nwaves = gridDim.x * 4u;
+    const unsigned nsl = nfr / 64u;
+    unsigned acc = 0;
+    for (unsigned s = wave; s < nsl; s += nwaves) {
+        const unsigned f = s * 64u + lane;
+        unsigned o = f, l = 64;
+        if (MODE & 1) { o = off64[f]; l = len[f]; }
+        u32x4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int fr = 16 * j + (lane >> 2);
+            const unsigned fo = __shfl(o, fr, 64);
+            v[j] = ld<false>(reinterpret_cast<const u32x4 *>(buf + (size_t)fo * 64u + (lane & 3) * 16));
+        }
+        unsigned t = l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t += v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+        if (MODE & 2) rec[f] = make_uint4(t, t + 1, t + 2, t + 3);
+        acc += t;
+    }
+    out[blockIdx.x * 256u + threadIdx.x] = acc;
+}
+
 template <typename F>
 static void timeit(const char *name, double bytes, F launch)
 {
@@ -114,7 +147,7 @@ int main()
     const int maxg = ncu * 32;
     CK(hipMalloc(&out, (size_t)maxg * 256 * sizeof(unsigned)));
     const size_t n16_a = (size_t)nfr * 1500u / 16u;  // the algorithmic byte count of C3
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < 1; ++rep) {
         for (int g : {ncu * 4, ncu * 8, ncu * 16}) {
             char nm[64];
             snprintf(nm, sizeof nm, "flat_def_u4_g%d", g);
@@ -129,6 +162,42 @@ int main()
             timeit(nm, nfr * 1500.0, [&] { frames<false, 1536><<<g, 256>>>(buf, nfr, out); });
             snprintf(nm, sizeof nm, "fr1504_nt_g%d", g);
             timeit(nm, nfr * 1500.0, [&] { frames<true, 1504><<<g, 256>>>(buf, nfr, out); });
+        }
+    }
+    {
+        // C2: 2^20 x 64 B frames per launch, 16 rotating copies (1 GiB)
+        const unsigned n2 = 1u << 20;
+        const int ncopy = 16;
+        uint8_t *f2;
+        unsigned *o2;
+        unsigned short *l2;
+        uint4 *r2;
+        CK(hipMalloc(&f2, (size_t)n2 * 64u * ncopy));
+        CK(hipMemset(f2, 3, (size_t)n2 * 64u * ncopy));
+        CK(hipMalloc(&o2, (size_t)n2 * 4u * ncopy));
+        CK(hipMalloc(&l2, (size_t)n2 * 2u * ncopy));
+        CK(hipMalloc(&r2, (size_t)n2 * 16u));
+        std::vector<unsigned> ho(n2);
+        for (unsigned i = 0; i < n2; ++i) ho[i] = i;
+        std::vector<unsigned short> hl(n2, 64);
+        for (int c = 0; c < ncopy; ++c) {
+            CK(hipMemcpy(o2 + (size_t)c * n2, ho.data(), n2 * 4u, hipMemcpyHostToDevice));
+            CK(hipMemcpy(l2 + (size_t)c * n2, hl.data(), n2 * 2u, hipMemcpyHostToDevice));
+        }
+        int it = 0;
+        for (int g : {ncu * 3, ncu * 4, ncu * 8}) {
+            char nm[64];
+            auto run = [&](auto m) {
+                constexpr int M = decltype(m)::value;
+                const int c = it++ % ncopy;
+                small<M><<<g, 256>>>(f2 + (size_t)c * n2 * 64u, o2 + (size_t)c * n2, l2 + (size_t)c * n2, n2, r2, out);
+            };
+            snprintf(nm, sizeof nm, "c2_frames_g%d", g);
+            timeit(nm, n2 * 64.0, [&] { run(std::integral_constant<int, 0>{}); });
+            snprintf(nm, sizeof nm, "c2_desc_g%d", g);
+            timeit(nm, n2 * 64.0, [&] { run(std::integral_constant<int, 1>{}); });
+            snprintf(nm, sizeof nm, "c2_desc_rec_g%d", g);
+            timeit(nm, n2 * 64.0, [&] { run(std::integral_constant<int, 3>{}); });
         }
     }
     CK(hipDeviceSynchronize());
