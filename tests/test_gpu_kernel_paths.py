@@ -1,0 +1,125 @@
+"""GPU parity for the rx kernel's internal paths that small batches on a full grid never
+reach:
+
+* the per-wave LDS record ring filling up and flushing mid-stream (a wave sees more
+  slices than the ring holds) -- forced with a one- or three-workgroup grid;
+* runs of all-small slices (the prefetched small-slice pipeline) starting, continuing and
+  ending next to class-path slices;
+* the per-lane last-flow cache: a lane repeating its previous tuple (exact TCB, listener,
+  no PCB, NULL slot before the listener) skips the probe and must give the same record.
+
+Everything is compared bit-exact, records and counters, with the oracle.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import pktgen
+import rxg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=[1, 3])
+def small_grid_engine(request):
+    """A context whose rx grid is `param` workgroups (RXG_MAX_BLOCKS is read when the
+    context is created): 4 or 12 waves, so each wave walks many slices."""
+    old = os.environ.get("RXG_MAX_BLOCKS")
+    os.environ["RXG_MAX_BLOCKS"] = str(request.param)
+    try:
+        eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20)
+    finally:
+        if old is None:
+            del os.environ["RXG_MAX_BLOCKS"]
+        else:
+            os.environ["RXG_MAX_BLOCKS"] = old
+    yield eng
+    eng.close()
+
+
+def _small_frame(rng, src, sport, dport, flags=0x10):
+    # <= 64 bytes: 54 B of headers + 0..10 payload bytes
+    return pktgen.frame(src_ip=src, sport=sport, dport=dport, flags=flags,
+                        payload=rng.randbytes(rng.randrange(0, 11)))
+
+
+def _batch(seed):
+    """Stretches of slices (64 frames each) of three kinds, long enough that every wave of
+    a 1- or 3-workgroup grid meets runs of each kind:
+      'same'  : one tuple per lane repeated slice after slice (flow-cache hits), the tuple
+                cycling through exact / listener / no-PCB / NULL-slot cases;
+      'small' : random <= 64 B frames of random flows (cache misses, truncated frames);
+      'mixed' : the random parity mixture (all size classes, malformed frames)."""
+    rng = random.Random(seed)
+    rows, flows, special = pktgen.parity_table(rng, 300)
+    cases = [
+        flows[3],                                        # exact hit
+        (pktgen.ip4(10, 99, 1, 1), 7777, 80),            # listener :80, non-SYN -> RST
+        (pktgen.ip4(10, 99, 1, 2), 7778, 8080),          # listener :8080 behind a NULL slot
+        (pktgen.ip4(10, 99, 1, 3), 7779, 9999),          # no PCB -> RST
+        special["dup"],                                  # duplicate tuple: lowest index
+        special["hostdst"],                              # host-order dst: pass 1 misses
+    ]
+    frames = []
+    plan = ["same"] * 24 + ["mixed"] * 8 + ["small"] * 20 + ["same"] * 16 + ["mixed"] * 4 + \
+           ["small", "mixed"] * 10 + ["same"] * 40 + ["mixed"] * 12
+    lane_case = [rng.randrange(len(cases)) for _ in range(64)]
+    for kind in plan:
+        if kind == "same":
+            if rng.random() < 0.3:  # some lanes change flow between slices
+                for _ in range(8):
+                    lane_case[rng.randrange(64)] = rng.randrange(len(cases))
+            for lane in range(64):
+                src, sport, dport = cases[lane_case[lane]]
+                flags = 0x02 if (lane % 5 == 0) else 0x10
+                frames.append(_small_frame(rng, src, sport, dport, flags))
+        elif kind == "small":
+            for _ in range(64):
+                src, sport, dport = rng.choice(flows)
+                f = _small_frame(rng, src, sport, dport)
+                if rng.random() < 0.1:
+                    f = f[:rng.randrange(0, len(f) + 1)]  # truncated
+                frames.append(f)
+        else:
+            frames.extend(pktgen.random_frame(rng, flows, special) for _ in range(64))
+    return rows, frames
+
+
+def _check(engine, rows, frames, rec_kind):
+    arena, off, lens = pktgen.pack_arena(frames)
+    tcb, live = pktgen.table_arrays(rows)
+    engine.tcb_load(tcb, live)
+    engine.counters_reset()
+    got = engine.rx_arena(arena, off, lens, rec_kind)
+    cnt = engine.counters()
+    exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+    if rec_kind == rxg.REC16:
+        exp = exp["c"]
+    if got.tobytes() != exp.tobytes():
+        g = got if rec_kind == rxg.REC16 else got["c"]
+        e = exp if rec_kind == rxg.REC16 else exp["c"]
+        gb = g.view(np.uint8).reshape(len(frames), -1)
+        eb = e.view(np.uint8).reshape(len(frames), -1)
+        bad = np.nonzero((gb != eb).any(axis=1))[0]
+        i = int(bad[0])
+        raise AssertionError(f"records differ at {len(bad)} frames, first {i} (slice {i // 64}, "
+                             f"lane {i % 64}, len {len(frames[i])}): got {g[i]} exp {e[i]}")
+    assert np.array_equal(cnt, ecnt), (cnt, ecnt)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+@pytest.mark.parametrize("rec_kind", [rxg.REC16, rxg.REC48])
+def test_many_slices_per_wave(small_grid_engine, seed, rec_kind):
+    rows, frames = _batch(seed)
+    _check(small_grid_engine, rows, frames, rec_kind)
+
+
+def test_partial_last_slice_after_small_run(small_grid_engine):
+    """A run of full small slices followed by a partial last slice (n % 64 != 0): the run
+    must stop before it (the partial slice takes the class path)."""
+    rows, frames = _batch(23)
+    frames = frames[:64 * 30 + 37]
+    _check(small_grid_engine, rows, frames, rxg.REC48)
