@@ -309,8 +309,8 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3_1500B_1Kflows", choices=sorted(WORKLOADS))
     ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU per step")
     ap.add_argument("--rec", type=int, default=16, choices=[16, 48])
