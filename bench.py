@@ -266,6 +266,27 @@ def payload_leg(eng, wl, steps, warmup):
             d.free()
 
 
+def tx_leg(eng, wl, steps, warmup):
+    """tx checksum generate (rxg_tx_cksum_dev, what ip_out computes,
+    ip.c:97-118) over the device-resident batch of the workload, in place.  The frames'
+    checksums are already the generated values, so the batch stays valid.  Algorithmic
+    bytes per launch = the frame bytes read (the 4 checksum bytes written per frame are
+    included in the traffic, not in the unit)."""
+    b = wl.batches[0]
+    for _ in range(warmup):
+        eng.tx_cksum_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, wl.n)
+    evs = [(eng.event(), eng.event()) for _ in range(steps)]
+    for a, e in evs:
+        eng.record(a)
+        eng.tx_cksum_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, wl.n)
+        eng.record(e)
+    eng.sync()
+    k = float(np.mean([eng.elapsed_ms(a, e) for a, e in evs])) / 1e3
+    return {"kernel_us": round(k * 1e6, 2), "mpps": round(wl.n / k / 1e6, 1),
+            "achieved_GBps": round(wl.bytes_per_batch / k / 1e9, 1),
+            "roofline_frac": round(wl.bytes_per_batch / k / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
     """The oracle's faithful restatement of the reference rx path (port), on one host
     core, over a bounded sample of the same workload (first sample_n frames)."""
@@ -377,6 +398,7 @@ def main():
             }
             lw.free()
         legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
+        legs["tx_generate_dev"] = tx_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)
         legs["c5_bidir_copy_inclusive"] = c5_leg(eng, args.frames, max(3, args.steps // 4), 1, device,
                                                  seed)

@@ -566,11 +566,22 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
     F.h1 = h1;
     F.h2 = h2;
     if constexpr (TX) {
-        // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118); frames of
-        // these classes are longer than 64 bytes
-        if (leader) {
-            *reinterpret_cast<uint16_t *>(fp + 24) = (uint16_t)bswap16(ip_ck);
-            *reinterpret_cast<uint16_t *>(fp + 50) = (uint16_t)bswap16(tcp_ck);
+        // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118).  Frames of
+        // these classes are longer than 64 bytes: the group writes the frame's whole first
+        // 64-byte line (chunks 0-3, as loaded, with the two checksum fields set) rather
+        // than two 2-byte stores, so HBM sees full-line writes, not partial-line ones
+        // (C3 tx 327 -> 310 us; holding the writes until the next round's loads are
+        // issued measured slower, 322).
+        const uint32_t ck2 = lane_read(bswap16(ip_ck) | (bswap16(tcp_ck) << 16), gbase);
+#pragma unroll
+        for (int j = 0; j < NLOAD && j * LPF < 4; ++j) {
+            const int c = gl + j * LPF;
+            if (active && c < 4) {
+                uint4 q = make_uint4(d[j][0], d[j][1], d[j][2], d[j][3]);
+                if (c == 1) q.z = (q.z & 0xFFFF0000u) | (ck2 & 0xFFFFu);        // bytes 24-25
+                if (c == 3) q.x = (q.x & 0x0000FFFFu) | (ck2 & 0xFFFF0000u);    // bytes 50-51
+                *reinterpret_cast<uint4 *>(fp + 16 * c) = q;
+            }
         }
     }
     return F;
