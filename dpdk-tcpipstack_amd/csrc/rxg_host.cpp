@@ -19,6 +19,7 @@
 #include "rxg.h"
 #include "rxg_common.h"
 #include "rxg_kernels.h"
+#include "rxg_opqueue.h"
 
 using namespace rxg;
 
@@ -62,6 +63,9 @@ struct rxg_ctx {
     int variant = 0;  // RXG_VARIANT: experiment kernels (tools/kbench only)
     int nocount = 0;  // RXG_NOCOUNT: experiment only, skip the counter reduction
     int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather experiment kernels
+
+    // tcbs[] writes posted by other threads (rxg_tcb_post), applied by the rx thread
+    rxg::MpscRing<rxg_tcb_op> posted{RXG_TCB_QUEUE_CAP};
 
     // host mirror of tcbs[0..ntcb)
     std::vector<rxg_tcb_tuple> tcb;
@@ -324,9 +328,46 @@ extern "C" int32_t rxg_tcb_count(rxg_ctx *c) { return c ? (int32_t)c->tcb.size()
 static inline bool port_ok(int32_t p) { return p >= 0 && p <= 0xFFFF; }
 
 // Rebuild the device mirror from the host mirror (DESIGN.md §TCB mirror).
+extern "C" int rxg_tcb_post(rxg_ctx *c, const rxg_tcb_op *op)
+{
+    if (!c || !op) return fail(-EINVAL, "rxg_tcb_post: NULL argument");
+    if (op->kind < RXG_TCB_OP_UPSERT || op->kind > RXG_TCB_OP_SET_STATE)
+        return fail(-EINVAL, "rxg_tcb_post: kind %u", op->kind);
+    if (!c->posted.push(*op)) return fail(-EAGAIN, "rxg_tcb_post: queue full (%u ops)", c->posted.capacity());
+    return 0;
+}
+
+extern "C" int rxg_tcb_drain(rxg_ctx *c)
+{
+    if (!c) return fail(-EINVAL, "rxg_tcb_drain: ctx NULL");
+    int applied = 0, first_err = 0;
+    rxg_tcb_op op;
+    while (c->posted.pop(op)) {
+        int rc = 0;
+        if (op.kind == RXG_TCB_OP_UPSERT) rc = rxg_tcb_upsert(c, op.idx, &op.tuple);
+        else if (op.kind == RXG_TCB_OP_REMOVE) rc = rxg_tcb_remove(c, op.idx);
+        else rc = rxg_tcb_set_state(c, op.idx, op.state);
+        if (rc && !first_err) first_err = rc;
+        ++applied;
+    }
+    return first_err ? first_err : applied;
+}
+
+static int tcb_push(rxg_ctx *c);
+
+// Burst boundary (rx thread): posted writes first, then the device mirror.
 extern "C" int rxg_tcb_sync(rxg_ctx *c)
 {
     if (!c) return fail(-EINVAL, "rxg_tcb_sync: ctx NULL");
+    const int rc = rxg_tcb_drain(c);
+    if (rc < 0) return rc;
+    return c->dirty ? tcb_push(c) : 0;
+}
+
+// Rebuild the device mirror from the host mirror (no draining: inside a replay only the rx
+// thread's own writes count, sequentially).
+static int tcb_push(rxg_ctx *c)
+{
     if (!c->dirty) return 0;
     int rc = set_device(c);
     if (rc) return rc;
@@ -474,7 +515,7 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
         return fail(-EINVAL, "rxg_rx_burst_dev: NULL device pointer");
     int rc = set_device(c);
     if (rc) return rc;
-    if (c->dirty && (rc = rxg_tcb_sync(c))) return rc;
+    if ((rc = rxg_tcb_sync(c))) return rc;
     if ((rc = arp_sync(c))) return rc;
     c->arp_since_burst.clear();
     c->last_frames = (const uint8_t *)b->frames;
@@ -732,7 +773,7 @@ static int reclassify(rxg_ctx *c, const std::vector<uint32_t> &sel, std::vector<
         return fail(-EINVAL, "rxg_rx_replay: no burst on this context to re-classify against");
     if ((rc = ensure(c->d_sel, sel.size() * 4))) return rc;
     if ((rc = ensure(c->d_fix, sel.size() * sizeof(rxg_rec16)))) return rc;
-    if (c->dirty && (rc = rxg_tcb_sync(c))) return rc;
+    if (c->dirty && (rc = tcb_push(c))) return rc;
     HIP_OK(hipMemcpyAsync(c->d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, c->stream));
     LaunchRx L;
     std::memset(&L, 0, sizeof L);

@@ -71,6 +71,16 @@ class TcbTuple(C.Structure):
                 ("identifier", C.c_uint16)]
 
 
+TCB_OP_UPSERT, TCB_OP_REMOVE, TCB_OP_SET_STATE = 1, 2, 3
+TCB_QUEUE_CAP = 65536
+
+
+class TcbOp(C.Structure):
+    """rxg_tcb_op (include/rxg.h): a tcbs[] write posted from another thread."""
+    _fields_ = [("kind", C.c_uint32), ("idx", C.c_int32), ("tuple", TcbTuple), ("state", C.c_uint8),
+                ("pad", C.c_uint8 * 3)]
+
+
 class DevBatch(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("off64", C.c_void_p), ("len", C.c_void_p),
                 ("n", C.c_uint32), ("rec_kind", C.c_uint32), ("out", C.c_void_p)]
@@ -151,6 +161,8 @@ def load_library(path: str = LIB_PATH):
         "rxg_tcb_load": (C.c_int, [vp, vp, vp, i32]),
         "rxg_tcb_sync": (C.c_int, [vp]),
         "rxg_tcb_count": (i32, [vp]),
+        "rxg_tcb_post": (C.c_int, [vp, C.POINTER(TcbOp)]),
+        "rxg_tcb_drain": (C.c_int, [vp]),
         "rxg_arp_load": (C.c_int, [vp, vp, u32]),
         "rxg_arp_learned": (C.c_int, [vp, u32]),
         "rxg_arp_count": (i32, [vp]),
@@ -366,6 +378,24 @@ class Engine:
 
     def tcb_count(self) -> int:
         return _lib.rxg_tcb_count(self.ctx)
+
+    # --- writes from other threads (rxg_tcb_post: lock-free, applied at the next burst)
+    def tcb_post_upsert(self, idx: int, dport: int, sport: int, ipv4_dst: int, ipv4_src: int,
+                        state: int, identifier: int = 0) -> int:
+        op = TcbOp(TCB_OP_UPSERT, idx, TcbTuple(dport, sport, ipv4_dst, ipv4_src, state, 0, identifier), 0)
+        return _lib.rxg_tcb_post(self.ctx, C.byref(op))
+
+    def tcb_post_remove(self, idx: int) -> int:
+        return _lib.rxg_tcb_post(self.ctx, C.byref(TcbOp(TCB_OP_REMOVE, idx)))
+
+    def tcb_post_set_state(self, idx: int, state: int) -> int:
+        return _lib.rxg_tcb_post(self.ctx, C.byref(TcbOp(TCB_OP_SET_STATE, idx, TcbTuple(), state)))
+
+    def tcb_drain(self) -> int:
+        rc = _lib.rxg_tcb_drain(self.ctx)
+        if rc < 0:
+            _check(rc, "rxg_tcb_drain")
+        return rc
 
     # --- ARP mirror (ip.c:30-32 learn, arp.c add_mac)
     def arp_load(self, ips):

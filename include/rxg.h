@@ -213,6 +213,29 @@ int rxg_tcb_sync(rxg_ctx *ctx);
 /* Current Ntcb of the mirror. */
 int32_t rxg_tcb_count(rxg_ctx *ctx);
 
+/* Writes from other threads.  The calls above belong to the rx thread (the one running
+   bursts and rxg_rx_replay, whose tcpswitch handlers write tcbs[] on the reference's rx
+   lcore).  The reference's socket API writes tcbs[] from the application lcore, unlocked
+   against the rx loop (alloc_tcb tcp_tcb.c:34-106, socket_bind socket_interface.c:80-83,
+   socket_connect :329-332); its mirror calls go through rxg_tcb_post instead: a lock-free
+   multi-producer queue the rx thread drains, in claim order, at the start of the next
+   burst (rxg_rx_burst, rxg_rx_burst_dev, rxg_ether_in) or rxg_tcb_sync / rxg_tcb_drain,
+   so a burst never sees a half-applied write.  Not drained during rxg_rx_replay. */
+enum rxg_tcb_op_kind { RXG_TCB_OP_UPSERT = 1, RXG_TCB_OP_REMOVE = 2, RXG_TCB_OP_SET_STATE = 3 };
+typedef struct rxg_tcb_op {
+    uint32_t kind;        /* enum rxg_tcb_op_kind                                   */
+    int32_t idx;          /* tcbs[] index                                           */
+    rxg_tcb_tuple tuple;  /* RXG_TCB_OP_UPSERT                                      */
+    uint8_t state;        /* RXG_TCB_OP_SET_STATE                                   */
+    uint8_t pad[3];
+} rxg_tcb_op;
+#define RXG_TCB_QUEUE_CAP 65536u
+/* Any thread.  -EAGAIN when RXG_TCB_QUEUE_CAP posts are waiting (nothing queued then). */
+int rxg_tcb_post(rxg_ctx *ctx, const rxg_tcb_op *op);
+/* rx thread: apply every posted write now.  Returns how many were applied, or the first
+   failing write's negative errno (the later ones are still applied). */
+int rxg_tcb_drain(rxg_ctx *ctx);
+
 /* ARP mirror (optional).  The reference keeps an IP -> MAC list that ip_in walks twice per
    packet (print_arp_table + get_mac, ip.c:26-32, arp.c:215-280).  Once a caller mirrors
    every add_mac (arp.c:282-317) with rxg_arp_learned, bursts flag each TCP packet whose

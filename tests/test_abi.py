@@ -56,9 +56,9 @@ def test_struct_layouts_match_header():
 #include <stddef.h>
 #include "rxg.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %d\n", sizeof(rxg_rec16), sizeof(rxg_rec48),
+  printf("%zu %zu %zu %zu %zu %zu %zu %d %zu\n", sizeof(rxg_rec16), sizeof(rxg_rec48),
          sizeof(rxg_tcb_tuple), sizeof(rxg_dev_batch), sizeof(rxg_pkt_view),
-         sizeof(rxg_synth_params), offsetof(rxg_rec48, src_mac), RXG_NCOUNTERS);
+         sizeof(rxg_synth_params), offsetof(rxg_rec48, src_mac), RXG_NCOUNTERS, sizeof(rxg_tcb_op));
   return 0;
 }'''
     tmp = os.path.join(ROOT, "build_abi_probe")
@@ -69,7 +69,7 @@ int main(void) {
                     os.path.join(tmp, "p")], check=True)
     got = subprocess.run([os.path.join(tmp, "p")], capture_output=True, text=True).stdout.split()
     assert [int(x) for x in got] == [16, 48, 20, C.sizeof(rxg.DevBatch), C.sizeof(rxg.PktView),
-                                     C.sizeof(rxg.SynthParams), 41, rxg.NCOUNTERS]
+                                     C.sizeof(rxg.SynthParams), 41, rxg.NCOUNTERS, C.sizeof(rxg.TcbOp)]
     assert rxg.REC48_DTYPE.fields["src_mac"][1] == 41
     assert "RXG_NCOUNTERS" in hdr
 
