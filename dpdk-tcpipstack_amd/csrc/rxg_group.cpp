@@ -1,0 +1,305 @@
+// rxg_group.cpp — several GPUs behind one rx loop.
+//
+// A group is one rxg context per device.  Every context holds a full replica of the TCB
+// mirror (tcbs[] writes are applied to all of them), a host-buffer burst is cut into one
+// contiguous shard per member and the shards run concurrently (one host thread per member,
+// each on its own device and stream), and the records come back in packet order.  The
+// replay then walks the members' shards in packet order: a handler's tcbs[] write, mirrored
+// through the group, reaches every member before that member's shard is replayed, and
+// rxg_rx_replay re-classifies the shard's affected packets as it does within one burst, so
+// the group is sequentially equivalent to ether_in over the whole burst.
+//
+// Built on the public C ABI only (include/rxg.h).
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rxg.h"
+#include "rxg_opqueue.h"
+
+struct rxg_group {
+    std::vector<rxg_ctx *> m;
+    std::vector<uint32_t> shard_off, shard_n;  // the last group burst's shards
+    uint32_t last_n = 0;
+    bool arp_on = false;   // the ARP mirror is in use (rxg_group_arp_load / _learned)
+    int32_t replaying = -1;  // member whose shard rxg_group_rx_replay is in, else -1
+    // posts from other threads: one queue for the group, so every member applies them in
+    // the same (claim) order and the replicas stay identical
+    rxg::MpscRing<rxg_tcb_op> posted{RXG_TCB_QUEUE_CAP};
+};
+
+namespace {
+
+thread_local char g_err[256];
+
+int gfail(int rc, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return rc;
+}
+
+// Apply f to every member; the first error is returned (its text copied to the group's
+// error), the others still run.
+template <typename F>
+int each(rxg_group *g, F f)
+{
+    int first = 0;
+    for (size_t i = 0; i < g->m.size(); ++i) {
+        const int rc = f(g->m[i]);
+        if (rc < 0 && !first) first = gfail(rc, "member %zu: %s", i, rxg_last_error());
+    }
+    return first;
+}
+
+// The caller's hand-off table, seen through the group during a replay: add_mac also tells
+// every member's ARP mirror, so a later member does not learn the same source again.
+struct Shim {
+    rxg_group *g;
+    const rxg_handoff_ops *o;
+};
+#define SHIM(u) (*(const Shim *)(u))
+void sh_free(void *u, void *m) { SHIM(u).o->free_mbuf(SHIM(u).o->user, m); }
+int sh_arp_in(void *u, void *m) { return SHIM(u).o->arp_in(SHIM(u).o->user, m); }
+int sh_get_mac(void *u, uint32_t ip, unsigned char *mac) { return SHIM(u).o->get_mac(SHIM(u).o->user, ip, mac); }
+int sh_add_mac(void *u, uint32_t ip, const unsigned char *mac)
+{
+    const int r = SHIM(u).o->add_mac(SHIM(u).o->user, ip, mac);
+    if (SHIM(u).g->arp_on)
+        for (rxg_ctx *c : SHIM(u).g->m) rxg_arp_learned(c, ip);
+    return r;
+}
+void sh_rst(void *u, void *ip, void *tcp) { SHIM(u).o->send_reset(SHIM(u).o->user, ip, tcp); }
+void sh_seg(void *u, int32_t idx, uint32_t seq, uint32_t ack) { SHIM(u).o->on_segment(SHIM(u).o->user, idx, seq, ack); }
+int sh_switch(void *u, int32_t idx, uint8_t st, void *tcp, void *ip, void *m)
+{
+    return SHIM(u).o->tcpswitch(SHIM(u).o->user, idx, st, tcp, ip, m);
+}
+#undef SHIM
+
+}  // namespace
+
+extern "C" int rxg_group_init(const int32_t *devices, uint32_t ndev, const rxg_config *cfg, rxg_group **out)
+{
+    if (!out || !devices || ndev == 0) return gfail(-EINVAL, "rxg_group_init: bad argument");
+    *out = nullptr;
+    rxg_group *g = new rxg_group();
+    for (uint32_t i = 0; i < ndev; ++i) {
+        rxg_config c = cfg ? *cfg : rxg_config{0, 0, 0, 0};
+        c.device = devices[i];
+        rxg_ctx *ctx = nullptr;
+        const int rc = rxg_init(&c, &ctx);
+        if (rc) {
+            for (rxg_ctx *x : g->m) rxg_fini(x);
+            delete g;
+            return rc;
+        }
+        g->m.push_back(ctx);
+    }
+    *out = g;
+    return 0;
+}
+
+extern "C" int rxg_group_fini(rxg_group *g)
+{
+    if (!g) return 0;
+    for (rxg_ctx *c : g->m) rxg_fini(c);
+    delete g;
+    return 0;
+}
+
+extern "C" uint32_t rxg_group_size(rxg_group *g) { return g ? (uint32_t)g->m.size() : 0u; }
+
+extern "C" rxg_ctx *rxg_group_member(rxg_group *g, uint32_t i)
+{
+    return (g && i < g->m.size()) ? g->m[i] : nullptr;
+}
+
+// ---------------------------------------------------------------- mirror broadcast ---
+extern "C" int rxg_group_tcb_upsert(rxg_group *g, int32_t idx, const rxg_tcb_tuple *t)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_tcb_upsert: group NULL");
+    return each(g, [&](rxg_ctx *c) { return rxg_tcb_upsert(c, idx, t); });
+}
+
+extern "C" int rxg_group_tcb_remove(rxg_group *g, int32_t idx)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_tcb_remove: group NULL");
+    return each(g, [&](rxg_ctx *c) { return rxg_tcb_remove(c, idx); });
+}
+
+extern "C" int rxg_group_tcb_set_state(rxg_group *g, int32_t idx, uint8_t state)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_tcb_set_state: group NULL");
+    return each(g, [&](rxg_ctx *c) { return rxg_tcb_set_state(c, idx, state); });
+}
+
+extern "C" int rxg_group_tcb_load(rxg_group *g, const rxg_tcb_tuple *tcbs, const uint8_t *live, int32_t ntcb)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_tcb_load: group NULL");
+    return each(g, [&](rxg_ctx *c) { return rxg_tcb_load(c, tcbs, live, ntcb); });
+}
+
+extern "C" int rxg_group_tcb_post(rxg_group *g, const rxg_tcb_op *op)
+{
+    if (!g || !op) return gfail(-EINVAL, "rxg_group_tcb_post: NULL argument");
+    if (op->kind < RXG_TCB_OP_UPSERT || op->kind > RXG_TCB_OP_SET_STATE)
+        return gfail(-EINVAL, "rxg_group_tcb_post: kind %u", op->kind);
+    return g->posted.push(*op) ? 0 : gfail(-EAGAIN, "rxg_group_tcb_post: %u posts waiting", g->posted.capacity());
+}
+
+extern "C" int rxg_group_tcb_drain(rxg_group *g)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_tcb_drain: group NULL");
+    int applied = 0, first = 0;
+    rxg_tcb_op op;
+    while (g->posted.pop(op)) {
+        int rc;
+        if (op.kind == RXG_TCB_OP_UPSERT)
+            rc = rxg_group_tcb_upsert(g, op.idx, &op.tuple);
+        else if (op.kind == RXG_TCB_OP_REMOVE)
+            rc = rxg_group_tcb_remove(g, op.idx);
+        else
+            rc = rxg_group_tcb_set_state(g, op.idx, op.state);
+        if (rc < 0 && !first) first = rc;  // the text is already in the group's error
+        ++applied;
+    }
+    return first ? first : applied;
+}
+
+extern "C" int rxg_group_arp_load(rxg_group *g, const uint32_t *ipv4_host, uint32_t n)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_arp_load: group NULL");
+    g->arp_on = true;
+    return each(g, [&](rxg_ctx *c) { return rxg_arp_load(c, ipv4_host, n); });
+}
+
+extern "C" int rxg_group_arp_learned(rxg_group *g, uint32_t ipv4_host)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_arp_learned: group NULL");
+    g->arp_on = true;
+    return each(g, [&](rxg_ctx *c) { return rxg_arp_learned(c, ipv4_host); });
+}
+
+extern "C" int rxg_group_arp_disable(rxg_group *g)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_arp_disable: group NULL");
+    g->arp_on = false;
+    return each(g, [&](rxg_ctx *c) { return rxg_arp_disable(c); });
+}
+
+extern "C" int rxg_group_rcv_set(rxg_group *g, int32_t idx, uint32_t cur_seq, uint32_t pairs_pending)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_rcv_set: group NULL");
+    return each(g, [&](rxg_ctx *c) { return rxg_rcv_set(c, idx, cur_seq, pairs_pending); });
+}
+
+// ------------------------------------------------------------------------- bursts ---
+extern "C" int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32_t n, uint32_t rec_kind,
+                                  void *out_host)
+{
+    if (!g || (n && (!pkts || !out_host))) return gfail(-EINVAL, "rxg_group_rx_burst: NULL argument");
+    if (rec_kind != RXG_REC16 && rec_kind != RXG_REC48)
+        return gfail(-EINVAL, "rxg_group_rx_burst: rec_kind %u", rec_kind);
+    {  // the posted writes, on every member, before any shard reads its mirror
+        const int rc = rxg_group_tcb_drain(g);
+        if (rc < 0) return rc;
+    }
+    const uint32_t k = (uint32_t)g->m.size();
+    const uint32_t per = (n + k - 1) / k;
+    g->shard_off.assign(k, 0);
+    g->shard_n.assign(k, 0);
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint32_t o = i * per < n ? i * per : n;
+        g->shard_off[i] = o;
+        g->shard_n[i] = (o + per < n ? o + per : n) - o;
+    }
+    g->last_n = n;
+    std::vector<int> rc(k, 0);
+    std::vector<std::string> err(k);
+    auto run = [&](uint32_t i) {
+        rc[i] = rxg_rx_burst(g->m[i], pkts + g->shard_off[i], g->shard_n[i], rec_kind,
+                             (uint8_t *)out_host + (size_t)g->shard_off[i] * rec_kind);
+        if (rc[i]) err[i] = rxg_last_error();  // thread-local in the member's thread
+    };
+    std::vector<std::thread> th;
+    for (uint32_t i = 1; i < k; ++i) th.emplace_back(run, i);
+    run(0);
+    for (auto &t : th) t.join();
+    for (uint32_t i = 0; i < k; ++i)
+        if (rc[i]) return gfail(rc[i], "member %u: %s", i, err[i].c_str());
+    return 0;
+}
+
+extern "C" int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, void *const *mbufs,
+                                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t stride)
+{
+    if (!g || !ops || (n && (!mbufs || !frames || !recs))) return gfail(-EINVAL, "rxg_group_rx_replay: NULL argument");
+    if (n != g->last_n) return gfail(-EINVAL, "rxg_group_rx_replay: n=%u but the last group burst had %u", n, g->last_n);
+    Shim sh{g, ops};
+    rxg_handoff_ops so{};
+    so.user = &sh;
+    so.free_mbuf = ops->free_mbuf ? sh_free : nullptr;
+    so.arp_in = ops->arp_in ? sh_arp_in : nullptr;
+    so.get_mac = ops->get_mac ? sh_get_mac : nullptr;
+    so.add_mac = ops->add_mac ? sh_add_mac : nullptr;
+    so.send_reset = ops->send_reset ? sh_rst : nullptr;
+    so.on_segment = ops->on_segment ? sh_seg : nullptr;
+    so.tcpswitch = ops->tcpswitch ? sh_switch : nullptr;
+    struct Guard {
+        rxg_group *g;
+        ~Guard() { g->replaying = -1; }
+    } guard{g};
+    for (size_t i = 0; i < g->m.size(); ++i) {
+        const uint32_t o = g->shard_off[i];
+        g->replaying = (int32_t)i;
+        // the member's mirror already holds every write the earlier shards' handlers made
+        // (they went through rxg_group_tcb_*); its replay re-classifies what they affect
+        const int rc = rxg_rx_replay(g->m[i], &so, mbufs + o, frames + o,
+                                     (const rxg_rec16 *)((const uint8_t *)recs + (size_t)o * stride), g->shard_n[i],
+                                     stride);
+        if (rc) return gfail(rc, "member %zu: %s", i, rxg_last_error());
+    }
+    return 0;
+}
+
+extern "C" int rxg_group_payload_take(rxg_group *g, int32_t idx, uint32_t seq, uint32_t length,
+                                      rxg_payload_msg *msg)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_payload_take: group NULL");
+    if (g->replaying < 0) return 0;
+    return rxg_payload_take(g->m[(size_t)g->replaying], idx, seq, length, msg);
+}
+
+extern "C" int32_t rxg_group_replaying(rxg_group *g) { return g ? g->replaying : -EINVAL; }
+
+// ----------------------------------------------------------------------- counters ---
+extern "C" int rxg_group_counters_reset(rxg_group *g)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_counters_reset: group NULL");
+    return each(g, [&](rxg_ctx *c) {
+        int rc = rxg_counters_reset(c, nullptr);
+        return rc ? rc : rxg_sync(c);
+    });
+}
+
+extern "C" int rxg_group_counters_read(rxg_group *g, uint64_t *out)
+{
+    if (!g || !out) return gfail(-EINVAL, "rxg_group_counters_read: NULL argument");
+    std::memset(out, 0, sizeof(uint64_t) * RXG_NCOUNTERS);
+    for (rxg_ctx *c : g->m) {
+        uint64_t v[RXG_NCOUNTERS];
+        const int rc = rxg_counters_read(c, v);
+        if (rc) return rc;
+        for (int k = 0; k < RXG_NCOUNTERS; ++k) out[k] += v[k];
+    }
+    return 0;
+}
+
+extern "C" const char *rxg_group_last_error(void) { return g_err; }

@@ -591,7 +591,11 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
         if (l) std::memcpy(c->h_arena + slot * 64u, (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off, l);
         slot += need;
     }
-    if (n == 0) return 0;
+    if (n == 0) {  // still a burst: posted writes drained, replay state reset
+        rxg_dev_batch e{};
+        e.rec_kind = rec_kind;
+        return rxg_rx_burst_dev(c, &e, nullptr);
+    }
     HIP_OK(hipMemcpyAsync(c->d_arena, c->h_arena, slot * 64u, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipMemcpyAsync(c->d_off, c->h_off, n * 4u, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipMemcpyAsync(c->d_len, c->h_len, n * 2u, hipMemcpyHostToDevice, c->stream));
@@ -699,6 +703,7 @@ extern "C" int rxg_payload_take(rxg_ctx *c, int32_t idx, uint32_t seq, uint32_t 
     const int64_t pos = c->replay_pos;
     if (pos < 0 || (uint64_t)pos >= c->pm_n || length == 0 || length > 0xFFFFu) return 0;
     if (c->pm_pending) {  // first take after the gather: fetch the burst's descriptors
+        if (int rc = set_device(c)) return rc;
         HIP_OK(hipEventSynchronize(c->pm_ev));
         if (c->pm_n > c->h_pm_cap) {
             if (c->h_pm) HIP_OK(hipHostFree(c->h_pm));
@@ -727,6 +732,7 @@ extern "C" int rxg_payload_take(rxg_ctx *c, int32_t idx, uint32_t seq, uint32_t 
 extern "C" int rxg_counters_reset(rxg_ctx *c, void *stream)
 {
     if (!c) return fail(-EINVAL, "rxg_counters_reset: ctx NULL");
+    if (int rc = set_device(c)) return rc;
     HIP_OK(hipMemsetAsync(c->counters, 0, kCounterBytes, pick(c, stream)));
     return 0;
 }
@@ -734,6 +740,7 @@ extern "C" int rxg_counters_reset(rxg_ctx *c, void *stream)
 extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
 {
     if (!c || !out) return fail(-EINVAL, "rxg_counters_read: NULL argument");
+    if (int rc = set_device(c)) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     std::vector<uint64_t> rows((size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS);
     HIP_OK(hipMemcpyAsync(rows.data(), c->counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
@@ -802,6 +809,9 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         return fail(-EINVAL, "rxg_rx_replay: NULL argument");
     if (stride != RXG_REC16 && stride != RXG_REC48) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
     if (n && c->last_n != n) return fail(-EINVAL, "rxg_rx_replay: n=%u but the last burst had %u frames", n, c->last_n);
+    // the re-classify launches and the counter correction run on this context's device
+    // (a group replays several contexts from one thread, rxg_group.cpp)
+    if (int rc = set_device(c)) return rc;
     struct PosGuard {
         rxg_ctx *c;
         ~PosGuard() { c->replay_pos = -1; }

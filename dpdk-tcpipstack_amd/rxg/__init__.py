@@ -193,6 +193,27 @@ def load_library(path: str = LIB_PATH):
         "rxg_event_record": (C.c_int, [vp, vp, vp]),
         "rxg_event_elapsed_ms": (C.c_int, [vp, vp, vp, C.POINTER(C.c_float)]),
         "rxg_event_destroy": (C.c_int, [vp, vp]),
+        "rxg_group_init": (C.c_int, [vp, u32, C.POINTER(Config), C.POINTER(vp)]),
+        "rxg_group_fini": (C.c_int, [vp]),
+        "rxg_group_size": (u32, [vp]),
+        "rxg_group_member": (vp, [vp, u32]),
+        "rxg_group_tcb_upsert": (C.c_int, [vp, i32, C.POINTER(TcbTuple)]),
+        "rxg_group_tcb_remove": (C.c_int, [vp, i32]),
+        "rxg_group_tcb_set_state": (C.c_int, [vp, i32, C.c_uint8]),
+        "rxg_group_tcb_load": (C.c_int, [vp, vp, vp, i32]),
+        "rxg_group_tcb_post": (C.c_int, [vp, C.POINTER(TcbOp)]),
+        "rxg_group_tcb_drain": (C.c_int, [vp]),
+        "rxg_group_arp_load": (C.c_int, [vp, vp, u32]),
+        "rxg_group_arp_learned": (C.c_int, [vp, u32]),
+        "rxg_group_arp_disable": (C.c_int, [vp]),
+        "rxg_group_rcv_set": (C.c_int, [vp, i32, u32, u32]),
+        "rxg_group_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
+        "rxg_group_rx_replay": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, vp, u32, u32]),
+        "rxg_group_payload_take": (C.c_int, [vp, i32, u32, u32, C.POINTER(PayloadMsg)]),
+        "rxg_group_replaying": (i32, [vp]),
+        "rxg_group_counters_reset": (C.c_int, [vp]),
+        "rxg_group_counters_read": (C.c_int, [vp, vp]),
+        "rxg_group_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -207,6 +228,12 @@ def load_library(path: str = LIB_PATH):
 def _check(rc: int, what: str):
     if rc != 0:
         msg = _lib.rxg_last_error().decode(errors="replace") if _lib else ""
+        raise RxgError(f"{what} failed ({rc}): {msg}")
+
+
+def _gcheck(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.rxg_group_last_error().decode(errors="replace") if _lib else ""
         raise RxgError(f"{what} failed ({rc}): {msg}")
 
 
@@ -317,12 +344,20 @@ class Engine:
         self.ctx = ctx.value
         self.device = device
 
+    @classmethod
+    def _member(cls, ctx: int, device: int) -> "Engine":
+        """A group member's context, owned by its Group (close() does not free it)."""
+        e = cls.__new__(cls)
+        e.ctx, e.device, e._borrowed = ctx, device, True
+        return e
+
     def close(self):
         if getattr(self, "ctx", None):
             for d in getattr(self, "_pg_bufs", ()):
                 d.free()
             self._pg_bufs = ()
-            _lib.rxg_fini(self.ctx)
+            if not getattr(self, "_borrowed", False):
+                _lib.rxg_fini(self.ctx)
             self.ctx = None
 
     def __enter__(self):
@@ -538,6 +573,119 @@ class Engine:
         ms = C.c_float()
         _check(_lib.rxg_event_elapsed_ms(self.ctx, a, b, C.byref(ms)), "rxg_event_elapsed_ms")
         return ms.value
+
+
+class Group:
+    """Several contexts behind one rx loop (include/rxg.h: rxg_group_*).  The mirror calls
+    go to every member; rx_burst shards a burst over the members and returns its records in
+    packet order; replay() replays the shards in packet order."""
+
+    def __init__(self, devices, max_batch: int = 0, max_bytes: int = 0):
+        load_library()
+        devs = (C.c_int32 * len(devices))(*devices)
+        cfg = Config(0, max_batch, max_bytes, 0)
+        g = C.c_void_p()
+        _gcheck(_lib.rxg_group_init(devs, len(devices), C.byref(cfg), C.byref(g)), "rxg_group_init")
+        self.g = g.value
+        self.members = [Engine._member(_lib.rxg_group_member(self.g, i), d) for i, d in enumerate(devices)]
+
+    def close(self):
+        if getattr(self, "g", None):
+            for m in self.members:
+                m.close()
+            _lib.rxg_group_fini(self.g)
+            self.g = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __len__(self):
+        return _lib.rxg_group_size(self.g)
+
+    def tcb_load(self, tcbs: np.ndarray, live: np.ndarray | None = None):
+        tcbs = np.ascontiguousarray(tcbs, dtype=TCB_DTYPE)
+        lv = None if live is None else np.ascontiguousarray(live, dtype=np.uint8)
+        _gcheck(_lib.rxg_group_tcb_load(self.g, _ptr(tcbs), None if lv is None else _ptr(lv), len(tcbs)),
+                "rxg_group_tcb_load")
+
+    def tcb_upsert(self, idx: int, dport: int, sport: int, ipv4_dst: int, ipv4_src: int,
+                   state: int, identifier: int = 0):
+        t = TcbTuple(dport, sport, ipv4_dst, ipv4_src, state, 0, identifier)
+        _gcheck(_lib.rxg_group_tcb_upsert(self.g, idx, C.byref(t)), "rxg_group_tcb_upsert")
+
+    def tcb_remove(self, idx: int):
+        _gcheck(_lib.rxg_group_tcb_remove(self.g, idx), "rxg_group_tcb_remove")
+
+    def tcb_set_state(self, idx: int, state: int):
+        _gcheck(_lib.rxg_group_tcb_set_state(self.g, idx, state), "rxg_group_tcb_set_state")
+
+    def tcb_post_upsert(self, idx: int, dport: int, sport: int, ipv4_dst: int, ipv4_src: int,
+                        state: int, identifier: int = 0) -> int:
+        op = TcbOp(TCB_OP_UPSERT, idx, TcbTuple(dport, sport, ipv4_dst, ipv4_src, state, 0, identifier), 0)
+        return _lib.rxg_group_tcb_post(self.g, C.byref(op))
+
+    def tcb_post_remove(self, idx: int) -> int:
+        return _lib.rxg_group_tcb_post(self.g, C.byref(TcbOp(TCB_OP_REMOVE, idx)))
+
+    def tcb_post_set_state(self, idx: int, state: int) -> int:
+        return _lib.rxg_group_tcb_post(self.g, C.byref(TcbOp(TCB_OP_SET_STATE, idx, TcbTuple(), state)))
+
+    def tcb_drain(self) -> int:
+        rc = _lib.rxg_group_tcb_drain(self.g)
+        if rc < 0:
+            _gcheck(rc, "rxg_group_tcb_drain")
+        return rc
+
+    def arp_load(self, ips):
+        a = np.ascontiguousarray(np.asarray(ips, dtype=np.uint32))
+        _gcheck(_lib.rxg_group_arp_load(self.g, _ptr(a) if len(a) else None, len(a)), "rxg_group_arp_load")
+
+    def arp_learned(self, ip: int):
+        _gcheck(_lib.rxg_group_arp_learned(self.g, ip & 0xFFFFFFFF), "rxg_group_arp_learned")
+
+    def arp_disable(self):
+        _gcheck(_lib.rxg_group_arp_disable(self.g), "rxg_group_arp_disable")
+
+    def rcv_set(self, idx: int, cur_seq: int, pairs_pending: bool):
+        _gcheck(_lib.rxg_group_rcv_set(self.g, idx, cur_seq & 0xFFFFFFFF, int(bool(pairs_pending))),
+                "rxg_group_rcv_set")
+
+    def rx_burst(self, frames: list[bytes], rec_kind: int = REC48) -> np.ndarray:
+        n = len(frames)
+        bufs = [C.create_string_buffer(f, len(f) + 1) for f in frames]
+        views = (PktView * max(n, 1))()
+        for i, b in enumerate(bufs):
+            views[i] = PktView(C.addressof(b), 0, len(frames[i]), 0)
+        dt = REC48_DTYPE if rec_kind == REC48 else REC16_DTYPE
+        out = np.zeros(n, dtype=dt)
+        _gcheck(_lib.rxg_group_rx_burst(self.g, views, n, rec_kind, _ptr(out) if n else None),
+                "rxg_group_rx_burst")
+        return out
+
+    def rx_replay(self, ops, mbufs, frames, recs, n: int, stride: int):
+        """rxg_group_rx_replay with ctypes arguments (HandoffOps, void* arrays, record pointer)."""
+        _gcheck(_lib.rxg_group_rx_replay(self.g, C.byref(ops), mbufs, frames, recs, n, stride),
+                "rxg_group_rx_replay")
+
+    def replaying(self) -> int:
+        return _lib.rxg_group_replaying(self.g)
+
+    def payload_take(self, idx: int, seq: int, length: int):
+        m = PayloadMsg()
+        rc = _lib.rxg_group_payload_take(self.g, idx, seq & 0xFFFFFFFF, length, C.byref(m))
+        _gcheck(min(rc, 0), "rxg_group_payload_take")
+        return rc == 1, int(m.arena_off)
+
+    def counters_reset(self):
+        _gcheck(_lib.rxg_group_counters_reset(self.g), "rxg_group_counters_reset")
+
+    def counters(self) -> np.ndarray:
+        out = np.zeros(NCOUNTERS, dtype=np.uint64)
+        _gcheck(_lib.rxg_group_counters_read(self.g, _ptr(out)), "rxg_group_counters_read")
+        return out
 
 
 def synthetic_tcb_table(nflows: int, dst_raw: int = None, dport: int = 80):

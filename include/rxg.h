@@ -460,6 +460,58 @@ int rxg_event_destroy(rxg_ctx *ctx, rxg_event *e);
 /* Last error text of this thread (static storage). */
 const char *rxg_last_error(void);
 
+/* ------------------------------------------------------------------------- */
+/* Groups: several GPUs behind one rx loop.  The reference   */
+/* runs one rx lcore calling ether_in per packet (main.c:391-399); a group     */
+/* keeps that single loop and spreads each burst over its members.            */
+/*  - every member holds a full replica of the TCB / ARP / receive-window      */
+/*    mirrors: the rxg_group_* mirror calls apply to all of them;             */
+/*  - rxg_group_rx_burst cuts the burst into one contiguous shard per member   */
+/*    (ceil(n/ndev) frames, so cfg->max_batch is per shard), runs the shards   */
+/*    concurrently (one host thread per member) and returns the records in     */
+/*    packet order;                                                            */
+/*  - rxg_group_rx_replay replays the shards in packet order.  Handlers mirror */
+/*    their tcbs[] writes with rxg_group_tcb_* (not the member calls), so a    */
+/*    later member's replay sees them and re-classifies what they affect: the  */
+/*    composition equals ether_in over the whole burst, as for one context.    */
+/* Members are plain contexts (rxg_group_member) for everything else: device    */
+/* batches, payload gathers, timing.  Group calls are made from the rx thread;  */
+/* rxg_group_tcb_post is the any-thread exception (member rxg_tcb_post is not  */
+/* used on a group: per-member queues could order two posts differently).      */
+/* ------------------------------------------------------------------------- */
+typedef struct rxg_group rxg_group;
+/* One context per devices[i] (the same device may repeat), each with *cfg's sizes. */
+int rxg_group_init(const int32_t *devices, uint32_t ndev, const rxg_config *cfg, rxg_group **out);
+int rxg_group_fini(rxg_group *g);
+uint32_t rxg_group_size(rxg_group *g);
+rxg_ctx *rxg_group_member(rxg_group *g, uint32_t i);
+int rxg_group_tcb_upsert(rxg_group *g, int32_t idx, const rxg_tcb_tuple *t);
+int rxg_group_tcb_remove(rxg_group *g, int32_t idx);
+int rxg_group_tcb_set_state(rxg_group *g, int32_t idx, uint8_t state);
+int rxg_group_tcb_load(rxg_group *g, const rxg_tcb_tuple *tcbs, const uint8_t *live, int32_t ntcb);
+/* Any thread: one lock-free queue for the whole group (the members apply posts in one
+   order), drained at the start of rxg_group_rx_burst or by rxg_group_tcb_drain. */
+int rxg_group_tcb_post(rxg_group *g, const rxg_tcb_op *op);
+int rxg_group_tcb_drain(rxg_group *g);
+int rxg_group_arp_load(rxg_group *g, const uint32_t *ipv4_host, uint32_t n);
+int rxg_group_arp_learned(rxg_group *g, uint32_t ipv4_host);
+int rxg_group_arp_disable(rxg_group *g);
+int rxg_group_rcv_set(rxg_group *g, int32_t idx, uint32_t cur_seq, uint32_t pairs_pending);
+int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32_t n, uint32_t rec_kind,
+                       void *out_host);
+int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, void *const *mbufs,
+                        void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
+/* rxg_payload_take on the member whose shard is being replayed (0 outside a replay);
+   each member's rxg_payload_gather_dev covers its own shard. */
+int rxg_group_payload_take(rxg_group *g, int32_t idx, uint32_t seq, uint32_t length, rxg_payload_msg *msg);
+/* Index of the member being replayed, -1 outside rxg_group_rx_replay. */
+int32_t rxg_group_replaying(rxg_group *g);
+int rxg_group_counters_reset(rxg_group *g);
+/* The members' counters summed. */
+int rxg_group_counters_read(rxg_group *g, uint64_t *out);
+/* Last error of a group call on this thread (member errors carry their text). */
+const char *rxg_group_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif
