@@ -71,6 +71,14 @@ def max_over_ranks(x: float, device) -> float:
     return float(t.item())
 
 
+def sum_over_ranks(x: float, device) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def barrier(device):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
@@ -157,9 +165,8 @@ def copy_inclusive_leg(eng, wl, steps, warmup, device):
     eng.sync()
     barrier(device)
     dt = max_over_ranks(time.perf_counter() - t0, device)
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    res = {"mpps": round(wl.n * steps * world / dt / 1e6, 2),
-           "gbs": round(wl.bytes_per_batch * steps * world / dt / 1e9, 2),
+    res = {"mpps": round(sum_over_ranks(wl.n, device) * steps / dt / 1e6, 2),
+           "gbs": round(sum_over_ranks(wl.bytes_per_batch, device) * steps / dt / 1e9, 2),
            "h2d_bytes_per_step": nb + wl.n * 6, "d2h_bytes_per_step": wl.n * wl.rec,
            "ms_per_step": round(dt / steps * 1e3, 3)}
     for a in (h_arena, h_off, h_len, h_out):
@@ -218,14 +225,14 @@ def c5_leg(eng, n, steps, warmup, device, seed):
     barrier(device)
     dt = max_over_ranks(time.perf_counter() - t0, device)
     c = merge_counters(eng.counters(), device)
-    world = dist.get_world_size() if dist.is_initialized() else 1
     rec = host["rec"].np[: n * 16].view(rxg.REC16_DTYPE)
+    n_all = int(sum_over_ranks(n, device))
+    b_all = sum_over_ranks(int(lens.astype(np.uint64).sum()) + int(tx_lens.astype(np.uint64).sum()), device)
     ok = bool((rec["verdict"] == rxg.V_DISPATCH).all() and (rec["tcp_cksum"] == 0).all()
-              and int(c[0]) == n * steps * world and int(c[8]) == 0)
+              and int(c[0]) == n_all * steps and int(c[8]) == 0)
     res = {"frames_per_dir_per_gpu": n, "flows": flows, "frame_mix": "imix 64/576/1500 7:4:1",
-           "mpps_per_direction": round(n * steps * world / dt / 1e6, 2),
-           "gbs_both_directions": round((int(lens.astype(np.uint64).sum()) + int(tx_lens.astype(np.uint64).sum()))
-                                        * steps * world / dt / 1e9, 2),
+           "mpps_per_direction": round(n_all * steps / dt / 1e6, 2),
+           "gbs_both_directions": round(b_all * steps / dt / 1e9, 2),
            "ms_per_step": round(dt / steps * 1e3, 3), "counters_ok": ok}
     for a in host.values():
         a.free()
@@ -287,7 +294,7 @@ def tx_leg(eng, wl, steps, warmup):
             "roofline_frac": round(wl.bytes_per_batch / k / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
+def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
     """The oracle's faithful restatement of the reference rx path (port), on one host
     core, over a bounded sample of the same workload (first sample_n frames)."""
     import oracle
@@ -317,6 +324,7 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
     oracle.arp_reset()
     mpps0, gbs0, pk0, dt0 = res["O0"]
     mpps2, gbs2, pk2, dt2 = res["O2"]
+    multi = cpu_replicas(arena, off, lens, tcb, live, cores, seconds * 0.5) if cores > 1 else None
     return {"value": round(gbs0, 6), "unit": "GB/s", "mpps": round(mpps0, 6), "cores": 1,
             "kind": "port",
             "sample": (f"faithful oracle (reference algorithms: byte-loop checksum, malloc+memcpy "
@@ -324,7 +332,32 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000):
                        f"walks, disabled-logger calls) built -O0 like tcp_ip_stack/Makefile:50, "
                        f"{pk0} frames of this workload in {dt0:.1f} s on 1 core; "
                        f"-O2 build: {mpps2:.4f} Mpps / {gbs2:.4f} GB/s"),
-            "o2": {"mpps": round(mpps2, 6), "gbs": round(gbs2, 6)}}
+            "o2": {"mpps": round(mpps2, 6), "gbs": round(gbs2, 6)},
+            "replicas": multi}
+
+
+def cpu_replicas(arena, off, lens, tcb, live, cores, seconds):
+    """one independent replica of the faithful oracle (-O0) per host
+    core, each its own process with private tables, on disjoint ranges of the sample.
+    Child processes only: nothing here touches the GPU."""
+    import subprocess
+    import tempfile
+    n = len(lens)
+    cores = max(1, min(cores, n))
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "sample.npz")
+        np.savez(path, arena=arena, off=off, lens=lens, tcb=tcb, live=live)
+        cuts = [n * k // cores for k in range(cores + 1)]
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "oracle", "replica.py"), path,
+                                   str(cuts[k]), str(cuts[k + 1]), str(seconds), "O0"],
+                                  stdout=subprocess.PIPE, text=True) for k in range(cores)]
+        outs = [json.loads(p.communicate(timeout=seconds + 120)[0]) for p in procs]
+    if any(p.returncode for p in procs):
+        return None
+    mpps = sum(o["frames"] / o["seconds"] for o in outs) / 1e6
+    gbs = sum(o["bytes"] / o["seconds"] for o in outs) / 1e9
+    return {"cores": cores, "mpps": round(mpps, 6), "gbs": round(gbs, 6), "opt": "O0",
+            "sample": f"{cores} processes, frames split {cuts[1] - cuts[0]}-ish each, {seconds:.1f} s"}
 
 
 def main():
@@ -338,6 +371,11 @@ def main():
     ap.add_argument("--no-legs", action="store_true", help="skip the 64 B / IMIX legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="replicas for the multi-core CPU leg (0: this process's CPU share, at most 16)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --frames per GPU; strong: --total-frames split over the GPUs")
+    ap.add_argument("--total-frames", type=int, default=1 << 23)
     args = ap.parse_args()
 
     rank, world, local = rank_env()
@@ -354,7 +392,11 @@ def main():
     stream = None  # the engine's own stream
 
     seed = shard_seed(0x5EED0001, rank)
-    wl = Workload(eng, args.workload, args.frames, seed, args.rec)
+    if args.scaling == "strong":  # fixed total, contiguous shares (SURVEY.md 8(d) "Scaling")
+        frames = args.total_frames // world + (1 if rank < args.total_frames % world else 0)
+    else:
+        frames = args.frames
+    wl = Workload(eng, args.workload, frames, seed, args.rec)
     tcb, live = rxg.synthetic_tcb_table(wl.flows)
     eng.tcb_load(tcb, live)
     eng.tcb_sync()
@@ -364,11 +406,12 @@ def main():
     elapsed_max = max_over_ranks(elapsed, device)
     merged = merge_counters(cnt, device)
 
-    total_frames = wl.n * args.steps * world
-    total_bytes = wl.bytes_per_batch * args.steps * world
+    total_frames = int(sum_over_ranks(wl.n, device)) * args.steps
+    total_bytes = int(sum_over_ranks(wl.bytes_per_batch, device)) * args.steps
     gbs = total_bytes / elapsed_max / 1e9
     mpps = total_frames / elapsed_max / 1e6
     k_avg_s = float(np.mean(kern_ms)) / 1e3
+    k_med_s = float(np.median(kern_ms)) / 1e3
     achieved = wl.bytes_per_batch / k_avg_s / 1e9
     C = {name: int(merged[i]) for i, name in enumerate(rxg.COUNTERS)}
     checks_ok = (C["rx"] == total_frames and C["bytes"] == total_bytes
@@ -380,33 +423,36 @@ def main():
         for name in ("c2_64B_1flow", "c4_imix_64Kflows"):
             if name == args.workload:
                 continue
-            lw = Workload(eng, name, args.frames, seed + 99, args.rec)
+            lw = Workload(eng, name, frames, seed + 99, args.rec)
             t2, l2 = rxg.synthetic_tcb_table(lw.flows)
             eng.tcb_load(t2, l2)
             e2, k2 = time_workload(eng, lw, args.steps, args.warmup, device, stream)
             e2 = max_over_ranks(e2, device)
             c2 = merge_counters(eng.counters(), device)
             ka = float(np.mean(k2)) / 1e3
+            ln = int(sum_over_ranks(lw.n, device)) * args.steps
+            lb = int(sum_over_ranks(lw.bytes_per_batch, device)) * args.steps
             legs[name] = {
-                "mpps": round(lw.n * args.steps * world / e2 / 1e6, 2),
-                "gbs": round(lw.bytes_per_batch * args.steps * world / e2 / 1e9, 2),
+                "mpps": round(ln / e2 / 1e6, 2),
+                "gbs": round(lb / e2 / 1e9, 2),
                 "kernel_us": round(ka * 1e6, 2),
                 "roofline_frac": round(lw.bytes_per_batch / ka / 1e9 / HBM_PEAK_GBS, 4),
                 "working_set_GiB": round(lw.copies * (lw.batches[0]["arena_bytes"]) / 2**30, 3),
-                "counters_ok": bool(int(c2[0]) == lw.n * args.steps * world
+                "counters_ok": bool(int(c2[0]) == ln
                                     and int(c2[7]) == 0 and int(c2[8]) == 0),
             }
             lw.free()
         legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
         legs["tx_generate_dev"] = tx_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)
-        legs["c5_bidir_copy_inclusive"] = c5_leg(eng, args.frames, max(3, args.steps // 4), 1, device,
+        legs["c5_bidir_copy_inclusive"] = c5_leg(eng, frames, max(3, args.steps // 4), 1, device,
                                                  seed)
         eng.tcb_load(tcb, live)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds)
+        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds, cores=cores)
 
     traffic, traffic_src = None, None
     tf = TRAFFIC_FILES.get((args.workload, wl.n, args.rec))
@@ -426,7 +472,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (device-generated Eth/IPv4/TCP frames, valid checksums, "
@@ -441,6 +487,7 @@ def main():
                          "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel_us": round(k_avg_s * 1e6, 2),
+                         "kernel_us_median": round(k_med_s * 1e6, 2),
                          "algorithmic_bytes_per_launch": wl.bytes_per_batch},
             "cpu_baseline": cpu,
             "counters_ok": bool(checks_ok),

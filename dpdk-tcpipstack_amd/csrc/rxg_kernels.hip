@@ -1249,24 +1249,16 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         return hipGetLastError();
     }
     if (L.mode == 16) {
-        switch (L.variant) {  // experiment variants (RXG_VARIANT); 0 = production
+        // experiment variants (RXG_VARIANT, scripts/kbench.py); 0 = production.  1-3: class
+        // subsets / plain loads; 8-10: C3 ablations (STRIP 2 no TCB probe, 4 no record
+        // store, 8 no phase B)
+        switch (L.variant) {
         case 1: hipLaunchKernelGGL((rx_kernel<16, 0x01, false>), dim3(blocks), dim3(256), 0, st, a); break;
         case 2: hipLaunchKernelGGL((rx_kernel<16, 0x20, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 3: hipLaunchKernelGGL((rx_kernel<16, 0xFF, false>), dim3(blocks), dim3(256), 0, st, a); break;
         case 8: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
         case 9: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         case 10: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 8>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 11: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 6>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 12: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 15>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 13: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 5>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 14: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 6>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 15: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 20: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 0, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 21: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 2, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 22: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 4, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 23: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 6, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 24: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 128, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 25: hipLaunchKernelGGL((rx_kernel<16, 0x01, false, 134, false, 11>), dim3(blocks), dim3(256), 0, st, a); break;
         default: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
     } else if (L.mode == 48) {

@@ -41,8 +41,9 @@ def _worker(rank, world, port, q):
     merged = bench.merge_counters(cnt, torch.device("cpu"))
     tmax = bench.max_over_ranks(float(rank + 1) * 0.5, torch.device("cpu"))
     seeds = [bench.shard_seed(0x5EED0001, r) for r in range(world)]
+    tsum = bench.sum_over_ranks(len(frames), torch.device("cpu"))
     bench.barrier(torch.device("cpu"))
-    q.put((rank, merged.tolist(), tmax, seeds))
+    q.put((rank, merged.tolist(), tmax, seeds, tsum))
     dist.destroy_process_group()
 
 
@@ -65,7 +66,22 @@ def test_two_rank_counter_merge_and_timing():
         arena, off, lens = pktgen.pack_arena(frames)
         tcb, live = pktgen.table_arrays(rows)
         total += oracle.rx_batch(arena, off, lens, tcb, live)[1]
-    for rank, merged, tmax, seeds in out:
+    for rank, merged, tmax, seeds, tsum in out:
         assert merged == total.tolist()
+        assert tsum == sum(len(_shard(r)[1]) for r in range(world))  # the value's numerator
         assert tmax == pytest.approx(1.0)  # max over ranks of (rank+1)/2
         assert len(set(seeds)) == world     # independent shard per rank
+
+
+def test_cpu_replicas_split_the_sample():
+    """bench.cpu_replicas: independent oracle processes over disjoint ranges of one sample."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "dpdk-tcpipstack_amd")]
+    import bench
+    import pktgen
+    rows, frames = pktgen.parity_set(seed=7, n=200)
+    arena, off, lens = pktgen.pack_arena(frames)
+    tcb, live = pktgen.table_arrays(rows)
+    r = bench.cpu_replicas(arena, off, lens, tcb, live, cores=2, seconds=0.5)
+    assert r is not None and r["cores"] == 2 and r["mpps"] > 0 and r["gbs"] > 0
