@@ -318,16 +318,19 @@ __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, ui
 //
 // Class of a frame by data_len: 0 <=64 | 1 <=128 | 2 <=256 | 3 <=512 | 8 <=768 | 4 <=1024 |
 // 5 <=1536 | 6 <=2048 | 7 more.  (<=768 runs 8 frames per round: IMIX's 576 B frames.)
+// Size classes (class id, then its lanes per frame x loads per lane in rx_kernel):
+// 513-576 is its own class (the IMIX 576-byte frame: 8 x 5 loads, 90 % of the chunks
+// used, instead of 8 x 6 at 75 %: C4 82.3 -> 80.6 us).
 __device__ __forceinline__ int size_class(uint32_t len)
 {
     return len <= 64u ? 0 : len <= 128u ? 1 : len <= 256u ? 2 : len <= 512u ? 3
-         : len <= 768u ? 8 : len <= 1024u ? 4 : len <= 1536u ? 5 : len <= 2048u ? 6 : 7;
+         : len <= 576u ? 10 : len <= 768u ? 8 : len <= 1024u ? 4 : len <= 1536u ? 5 : len <= 2048u ? 6 : 7;
 }
 
 // Smallest data_len of a class.
 constexpr int class_min_len(int c)
 {
-    return c == 0 ? 0 : c == 1 ? 65 : c == 2 ? 129 : c == 3 ? 257 : c == 8 ? 513 : c == 4 ? 769
+    return c == 0 ? 0 : c == 1 ? 65 : c == 2 ? 129 : c == 3 ? 257 : c == 10 ? 513 : c == 8 ? 577 : c == 4 ? 769
          : c == 5 ? 1025 : c == 6 ? 1537 : 2049;
 }
 
@@ -976,16 +979,24 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
                                            uint32_t &n_len, uint4 (&vb)[2][4], RecRing<MODE, RS> &ring,
                                            WaveCounters &wc, Rec &rec, FlowCache &fc, unsigned long long &bytes)
 {
-    uint32_t y_off, y_len;
-    load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len);
+    // Issue order (vmcnt retires in order): the TCB probe of this slice, then the next
+    // slice's frames, then the descriptors two slices ahead; waiting for the probe leaves
+    // both in flight.  (Probe after the frames: the probe's wait drained the prefetch,
+    // 64 B / 64 K flows 28.4 us.)
     const uint32_t s1 = s + nwaves;
     const bool nxt = s1 < nslices && s1 * 64u + 64u <= a.n && __ballot(n_len <= 64u) == ~0ull;
-    if (nxt) issue_small_slice<false>(a, n_off, n_len, lane, vb[1 - P]);
     uint32_t d[4][4];
     uint32_t *sf = ring.scratch(a, lane, 4096);
     transpose_small_slice(vb[P], lane, sf, d);
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
-    classify_store<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, wc, rec, fc);
+    const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
+    const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
+    const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
+    const Probe PR = ((STRIP & 2) || cached) ? probe_none() : probe_issue(a, true, F);
+    if (nxt) issue_small_slice<true>(a, n_off, n_len, lane, vb[1 - P]);
+    uint32_t y_off, y_len;
+    load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len);
+    classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PR, wc, rec, fc, cached);
     bytes += c_len;
     if (!(STRIP & 4)) {
         if (ring.n == RS) ring.flush(a, lane);
@@ -1048,7 +1059,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
                 // The two frame buffers alternate between the unrolled steps P = 0, 1 (a
                 // register copy of a load in flight would wait for it).
                 uint4 vb[2][4];
-                issue_small_slice<false>(a, c_off, c_len, lane, vb[0]);
+                issue_small_slice<true>(a, c_off, c_len, lane, vb[0]);
                 for (;;) {
                     if (!small_step<0, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
                                                              n_len, vb, ring, wc, rec, fcache, bytes))
@@ -1066,6 +1077,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT>(a, cls, off, len, lane, sf);
