@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Tx checksum-generate micro-benchmark: rxg_tx_cksum_dev over the C3 / C4 batch, one rxg
 context per RXG_MAX_BLOCKS value (0 = occupancy grid), interleaved rounds.
-  python scripts/txbench.py --grids 0,768 --workloads c3,c4"""
+  python scripts/txbench.py --grids 0,768 --workloads c3,c4
+A grid may name another librxg build as GRID:PATH (A/B of two builds in one process)."""
 import argparse
 import json
 import os
@@ -24,11 +25,21 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
-    engs = {}
+    engs, libs = {}, {}
+    main_lib = rxg.load_library()
     for g in args.grids.split(","):
-        os.environ["RXG_MAX_BLOCKS"] = g
+        grid, _, path = g.partition(":")
+        os.environ["RXG_MAX_BLOCKS"] = grid
+        lib = main_lib
+        if path:
+            rxg._lib = None
+            lib = rxg.load_library(path)
+        rxg._lib = lib
+        libs[g] = lib
         engs[g] = rxg.Engine(0)
+        rxg._lib = main_lib
     base = engs[args.grids.split(",")[0]]
+    rxg._lib = libs[args.grids.split(",")[0]]
     n = 1 << 20
     res = {}
     for w in args.workloads.split(","):
@@ -37,6 +48,7 @@ def main():
         nbytes = int(b["len"].download(np.uint16, n).astype(np.int64).sum())
         for r in range(args.rounds):
             for g, eng in engs.items():
+                rxg._lib = libs[g]
                 evs = [(eng.event(), eng.event()) for _ in range(args.iters)]
                 eng.tx_cksum_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n)
                 for a, e in evs:
