@@ -997,6 +997,32 @@ extern "C" int rxg_host_free_pinned(rxg_ctx *c, void *p)
     return 0;
 }
 
+// Zero-copy: page-lock caller memory (e.g. the mbuf pool's hugepages) and map it for the
+// device, so batches in it go to rxg_rx_burst_dev / rxg_tx_cksum_dev without a copy.
+extern "C" int rxg_host_register(rxg_ctx *c, void *p, uint64_t bytes, void **dev_alias)
+{
+    if (!c || !p || !bytes || !dev_alias) return fail(-EINVAL, "rxg_host_register: bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIP_OK(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+        (void)hipHostUnregister(p);
+        return fail(-EIO, "rxg_host_register: no device mapping for %p", p);
+    }
+    *dev_alias = d;
+    return 0;
+}
+
+extern "C" int rxg_host_unregister(rxg_ctx *c, void *p)
+{
+    if (!c || !p) return fail(-EINVAL, "rxg_host_unregister: bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIP_OK(hipHostUnregister(p));
+    return 0;
+}
+
 extern "C" int rxg_memcpy_h2d(rxg_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream)
 {
     if (!c) return fail(-EINVAL, "rxg_memcpy_h2d: ctx NULL");

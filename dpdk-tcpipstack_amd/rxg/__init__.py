@@ -185,6 +185,8 @@ def load_library(path: str = LIB_PATH):
         "rxg_dev_free": (C.c_int, [vp, vp]),
         "rxg_host_alloc_pinned": (C.c_int, [vp, u64, C.POINTER(vp)]),
         "rxg_host_free_pinned": (C.c_int, [vp, vp]),
+        "rxg_host_register": (C.c_int, [vp, vp, u64, C.POINTER(vp)]),
+        "rxg_host_unregister": (C.c_int, [vp, vp]),
         "rxg_memcpy_h2d": (C.c_int, [vp, vp, vp, u64, vp]),
         "rxg_memcpy_d2h": (C.c_int, [vp, vp, vp, u64, vp]),
         "rxg_memset_dev": (C.c_int, [vp, vp, C.c_int, u64, vp]),
@@ -372,6 +374,18 @@ class Engine:
 
     def sync(self):
         _check(_lib.rxg_sync(self.ctx), "rxg_sync")
+
+    def host_register(self, a: np.ndarray) -> int:
+        """Page-lock and map a host array for zero-copy batches; returns its device alias."""
+        d = C.c_void_p()
+        _check(_lib.rxg_host_register(self.ctx, _ptr(a), a.nbytes, C.byref(d)), "rxg_host_register")
+        return d.value
+
+    def host_unregister(self, a: np.ndarray):
+        _check(_lib.rxg_host_unregister(self.ctx, _ptr(a)), "rxg_host_unregister")
+
+    def stream_sync(self, stream):
+        _check(_lib.rxg_stream_sync(self.ctx, stream), "rxg_stream_sync")
 
     def alloc(self, nbytes: int) -> DevArray:
         return DevArray(self, nbytes)

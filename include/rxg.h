@@ -445,6 +445,15 @@ int rxg_dev_alloc(rxg_ctx *ctx, uint64_t bytes, void **out);
 int rxg_dev_free(rxg_ctx *ctx, void *p);
 int rxg_host_alloc_pinned(rxg_ctx *ctx, uint64_t bytes, void **out);
 int rxg_host_free_pinned(rxg_ctx *ctx, void *p);
+/* Zero-copy batches.  Host memory from rxg_host_alloc_pinned, or caller memory registered
+   here (e.g. the mbuf pool's hugepages: hipHostRegister, mapped), may be passed to
+   rxg_rx_burst_dev / rxg_tx_cksum_dev as `frames`, `off64`, `len` and `out` through its
+   device alias: the kernel reads (and for tx rewrites in place) the frames over PCIe, with
+   no staging copy.  rxg_tx_cksum_dev on host frames writes back only the rewritten first
+   line of each frame, not the frame (C5).  The alias is valid until
+   rxg_host_unregister. */
+int rxg_host_register(rxg_ctx *ctx, void *host, uint64_t bytes, void **dev_alias);
+int rxg_host_unregister(rxg_ctx *ctx, void *host);
 int rxg_memcpy_h2d(rxg_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
 int rxg_memcpy_d2h(rxg_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
 int rxg_memset_dev(rxg_ctx *ctx, void *dst, int value, uint64_t bytes, void *stream);
