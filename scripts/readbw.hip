@@ -134,7 +134,7 @@ static void timeit(const char *name, double bytes, F launch)
     fflush(stdout);
 }
 
-int main()
+int main(int argc, char **argv)
 {
     const unsigned nfr = 1u << 20;
     const size_t bytes = (size_t)nfr * 1536u;  // 1.61 GB
@@ -148,7 +148,12 @@ int main()
     CK(hipMalloc(&out, (size_t)maxg * 256 * sizeof(unsigned)));
     const size_t n16_a = (size_t)nfr * 1500u / 16u;  // the algorithmic byte count of C3
     for (int rep = 0; rep < 1; ++rep) {
-        for (int g : {ncu * 4, ncu * 8, ncu * 16}) {
+        std::vector<int> grids = {ncu * 4, ncu * 8, ncu * 16};
+        if (argc > 1) {  // workgroups per CU to sweep, e.g. "2 3 4"
+            grids.clear();
+            for (int i = 1; i < argc; ++i) grids.push_back(ncu * atoi(argv[i]));
+        }
+        for (int g : grids) {
             char nm[64];
             snprintf(nm, sizeof nm, "flat_def_u4_g%d", g);
             timeit(nm, n16_a * 16.0, [&] { flat<false, 4><<<g, 256>>>((const u32x4 *)buf, n16_a, out); });
