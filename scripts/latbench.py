@@ -20,7 +20,7 @@ import rxg  # noqa: E402
 
 
 def main():
-    sizes = [int(x) for x in (sys.argv[1:] or ["1", "32", "256", "4096", "65536"])]
+    sizes = [int(x) for x in (sys.argv[1:] or ["1", "32", "256", "1024", "4096", "65536"])]
     eng = rxg.Engine(0, max_batch=max(sizes), max_bytes=max(sizes) * 1536)
     lib = rxg.load_library()
     tcb, live = rxg.synthetic_tcb_table(1000)
