@@ -93,6 +93,29 @@ def test_no_gpu_fails_loudly():
         rxg.Engine(0)
 
 
+def test_group_and_null_arguments_fail_loudly():
+    """Group init without a GPU, and NULL arguments everywhere, return negative errno with a
+    message; nothing crashes and nothing falls back to the CPU."""
+    import ctypes as C
+    import torch
+    lib = rxg.load_library()
+    g = C.c_void_p()
+    if not torch.cuda.is_available():
+        devs = (C.c_int32 * 2)(0, 0)
+        assert lib.rxg_group_init(devs, 2, None, C.byref(g)) < 0
+        assert b"rxg_init" in lib.rxg_last_error() or lib.rxg_group_last_error()
+    assert lib.rxg_group_init(None, 0, None, C.byref(g)) == -22
+    assert b"bad argument" in lib.rxg_group_last_error()
+    assert lib.rxg_group_size(None) == 0 and lib.rxg_group_member(None, 0) is None
+    assert lib.rxg_group_tcb_post(None, None) == -22
+    assert lib.rxg_group_rx_burst(None, None, 0, 16, None) == -22
+    assert lib.rxg_group_replaying(None) == -22
+    d = C.c_void_p()
+    assert lib.rxg_host_register(None, None, 0, C.byref(d)) == -22
+    assert lib.rxg_tcb_post(None, None) == -22
+    assert lib.rxg_rx_burst(None, None, 0, 16, None) == -22
+
+
 def test_product_does_not_link_the_oracle():
     out = subprocess.run(["readelf", "-d", rxg.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
