@@ -25,6 +25,7 @@ struct rxg_group {
     std::vector<rxg_ctx *> m;
     std::vector<uint32_t> shard_off, shard_n;  // the last group burst's shards
     uint32_t last_n = 0;
+    bool burst_ok = false;  // the last group burst completed on every member
     bool arp_on = false;   // the ARP mirror is in use (rxg_group_arp_load / _learned)
     int32_t replaying = -1;  // member whose shard rxg_group_rx_replay is in, else -1
     // posts from other threads: one queue for the group, so every member applies them in
@@ -221,6 +222,7 @@ extern "C" int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32
         g->shard_n[i] = (o + per < n ? o + per : n) - o;
     }
     g->last_n = n;
+    g->burst_ok = false;
     std::vector<int> rc(k, 0);
     std::vector<std::string> err(k);
     auto run = [&](uint32_t i) {
@@ -234,6 +236,7 @@ extern "C" int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32
     for (auto &t : th) t.join();
     for (uint32_t i = 0; i < k; ++i)
         if (rc[i]) return gfail(rc[i], "member %u: %s", i, err[i].c_str());
+    g->burst_ok = true;
     return 0;
 }
 
@@ -242,6 +245,7 @@ extern "C" int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, voi
 {
     if (!g || !ops || (n && (!mbufs || !frames || !recs))) return gfail(-EINVAL, "rxg_group_rx_replay: NULL argument");
     if (n != g->last_n) return gfail(-EINVAL, "rxg_group_rx_replay: n=%u but the last group burst had %u", n, g->last_n);
+    if (!g->burst_ok) return gfail(-EINVAL, "rxg_group_rx_replay: the last group burst failed");
     Shim sh{g, ops};
     rxg_handoff_ops so{};
     so.user = &sh;

@@ -158,6 +158,11 @@ def test_group_posted_writes_and_errors():
         # a member error carries the member's text
         with pytest.raises(rxg.RxgError, match="member 0: .*index"):
             g.tcb_set_state(-3, 1)
-        # shards above max_batch fail the burst
+        # shards above max_batch fail the burst, and a replay of it is refused
+        big = [f] * (2 * (1 << 14) + 2)
         with pytest.raises(rxg.RxgError, match="max_batch"):
-            g.rx_burst([f] * (2 * (1 << 14) + 2), rxg.REC16)
+            g.rx_burst(big, rxg.REC16)
+        recs = np.zeros(len(big), dtype=rxg.REC16_DTYPE)
+        ptrs = (C.c_void_p * len(big))()
+        with pytest.raises(rxg.RxgError, match="last group burst failed"):
+            g.rx_replay(ops, ptrs, ptrs, recs.ctypes.data, len(big), 16)
