@@ -92,6 +92,7 @@ struct rxg_ctx {
     const uint32_t *last_off = nullptr;
     const uint16_t *last_len = nullptr;
     uint32_t last_n = 0;
+    bool burst_ok = false;  // the last burst was launched (device) / completed (host buffers)
     const uint8_t *last_recs = nullptr;  // the burst's records (device) and their size
     uint32_t last_stride = 0;
     DevBuf d_sel, d_fix;
@@ -519,6 +520,7 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
         return fail(-EINVAL, "rxg_rx_burst_dev: rec_kind %u", b->rec_kind);
     if (b->n && (!b->frames || !b->off64 || !b->len || !b->out))
         return fail(-EINVAL, "rxg_rx_burst_dev: NULL device pointer");
+    c->burst_ok = false;
     int rc = set_device(c);
     if (rc) return rc;
     if ((rc = rxg_tcb_sync(c))) return rc;
@@ -549,6 +551,7 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
     if (L.max_blocks == 0) L.max_blocks = 1024;
     L.variant = c->variant;
     HIP_OK(launch_rx(L, pick(c, stream)));
+    c->burst_ok = true;
     return 0;
 }
 
@@ -582,6 +585,7 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
         return fail(-EINVAL, "rxg_rx_burst: rec_kind %u", rec_kind);
     if (n > c->max_batch)
         return fail(-EINVAL, "rxg_rx_burst: n=%u exceeds max_batch=%u", n, c->max_batch);
+    c->burst_ok = false;
     int rc = set_device(c);
     if (rc) return rc;
     uint64_t slot = 0;
@@ -630,8 +634,10 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
         b.rec_kind = rec_kind;
         b.out = c->h_out;
         if ((rc = rxg_rx_burst_dev(c, &b, c->stream))) return rc;
+        c->burst_ok = false;  // until the records are back
         HIP_OK(hipStreamSynchronize(c->stream));
         std::memcpy(out_host, c->h_out, (size_t)n * rec_kind);
+        c->burst_ok = true;
         return 0;
     }
     HIP_OK(hipMemcpyAsync(c->d_arena, c->h_arena, slot * 64u, hipMemcpyHostToDevice, c->stream));
@@ -644,8 +650,10 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
     b.rec_kind = rec_kind;
     b.out = c->d_out;
     if ((rc = rxg_rx_burst_dev(c, &b, c->stream))) return rc;
+    c->burst_ok = false;  // until the records are back
     HIP_OK(hipMemcpyAsync(out_host, c->d_out, (size_t)n * rec_kind, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
+    c->burst_ok = true;
     return 0;
 }
 
@@ -846,6 +854,7 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         return fail(-EINVAL, "rxg_rx_replay: NULL argument");
     if (stride != RXG_REC16 && stride != RXG_REC48) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
     if (n && c->last_n != n) return fail(-EINVAL, "rxg_rx_replay: n=%u but the last burst had %u frames", n, c->last_n);
+    if (n && !c->burst_ok) return fail(-EINVAL, "rxg_rx_replay: the last burst on this context failed");
     // the re-classify launches and the counter correction run on this context's device
     // (a group replays several contexts from one thread, rxg_group.cpp)
     if (int rc = set_device(c)) return rc;

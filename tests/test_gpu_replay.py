@@ -202,3 +202,21 @@ def test_arp_learn_flag_and_replay(engine):
     engine.arp_disable()
     recs3 = engine.rx_burst(frames, rxg.REC16)
     assert not (recs3["flags"] & rxg.F_ARP_LEARN).any()
+
+
+def test_replay_refused_after_a_failed_burst(engine):
+    """A burst that fails after it started (staging full) leaves nothing to replay: the
+    replay of the same n is refused instead of replaying the previous burst's records."""
+    n = 45000
+    small = [pktgen.frame(sport=1000 + i % 50) for i in range(n)]
+    big = [pktgen.frame(sport=1000, payload=bytes(1446))] * n   # 67.5 MB > staging
+    recs = engine.rx_burst(small, rxg.REC16)
+    lib = rxg.load_library()
+    ops = rxg.HandoffOps()
+    bufs = [C.create_string_buffer(f, 64) for f in small[:1]] * n
+    ptrs = (C.c_void_p * n)(*[C.addressof(b) for b in bufs])
+    assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, n, 16) == 0
+    with pytest.raises(rxg.RxgError, match="staging arena"):
+        engine.rx_burst(big, rxg.REC16)
+    assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, n, 16) == -22
+    assert b"failed" in lib.rxg_last_error()
