@@ -344,7 +344,8 @@ typedef struct rxg_handoff_ops {
    changed slot; any packet that reached findtcb pass 2 after a slot was removed or NULL
    slots appeared) is re-classified on the GPU against the updated table before it is
    replayed, and the counters are corrected.  The composition rxg_rx_burst + rxg_rx_replay
-   therefore equals `for (i<n) ether_in(mbufs[i])`. */
+   therefore equals `for (i<n) ether_in(mbufs[i])`.  -EINVAL when n differs from the last
+   burst's or that burst failed after it started (nothing is replayed then). */
 int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
 
