@@ -364,7 +364,12 @@ def cpu_replicas(arena, off, lens, tcb, live, cores, seconds):
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "oracle", "replica.py"), path,
                                    str(cuts[k]), str(cuts[k + 1]), str(seconds), "O0"],
                                   stdout=subprocess.PIPE, text=True) for k in range(cores)]
-        outs = [json.loads(p.communicate(timeout=seconds + 120)[0]) for p in procs]
+        try:
+            outs = [json.loads(p.communicate(timeout=seconds + 120)[0]) for p in procs]
+        except (ValueError, subprocess.TimeoutExpired):  # a replica died: report no figure
+            for p in procs:
+                p.kill()
+            return None
     if any(p.returncode for p in procs):
         return None
     mpps = sum(o["frames"] / o["seconds"] for o in outs) / 1e6
