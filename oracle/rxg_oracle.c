@@ -55,15 +55,18 @@ static inline uint32_t le32(const uint8_t *b)
 /* ------------------------------------------------------------------ logger --- */
 
 /* logger.c:31-43: log_print tests LogFeature[f].Enable and the level; InitLogger leaves
-   every feature disabled (logger.c:9-23), so each call is a call + branch. */
+   every feature disabled (logger.c:9-23), so each call is a call + branch.  log_print lives
+   in its own translation unit in the reference, so no build of it can drop those calls:
+   noipa (and a feature table the optimiser cannot prove zero) keeps every call here too,
+   at -O2 as at -O0. */
 enum { ORC_LOG_ARP = 0, ORC_LOG_IP = 1, ORC_LOG_TCP = 2, ORC_LOG_TCB = 9, ORC_LOG_N = 11 };
 struct orc_logfeat {
     int level;
     uint8_t enable;
 };
-static struct orc_logfeat orc_logfeature[ORC_LOG_N];
+struct orc_logfeat orc_logfeature[ORC_LOG_N];
 
-__attribute__((noinline)) static void orc_log(int feature, int level, const char *fmt, ...)
+__attribute__((noinline, noipa)) static void orc_log(int feature, int level, const char *fmt, ...)
 {
     if (orc_logfeature[feature].enable == 1 && orc_logfeature[feature].level >= level) {
         va_list ap;
