@@ -74,8 +74,11 @@ def _post(engine, ops):
             assert engine.tcb_post_remove(i) == 0
 
 
-@pytest.mark.parametrize("seed", [101, 202])
-def test_random_bursts_equal_sequential_reference(engine, seed):
+@pytest.mark.parametrize("seed,arp", [(101, False), (202, False), (303, True)])
+def test_random_bursts_equal_sequential_reference(engine, seed, arp):
+    """arp: the ARP mirror is on (half the sources known up front); the replay's add_mac
+    calls must be the reference's ip_in learns (ip.c:30-32), first sighting in stream
+    order, across bursts."""
     rng = random.Random(seed)
     rows, frames = scenario(seed, n=2500)
     dst_raw = rows[0][2]
@@ -101,10 +104,23 @@ def test_random_bursts_equal_sequential_reference(engine, seed):
             exp.append((int(r["verdict"]), int(r["tcb_idx"]), int(r["state"])))
             if r["verdict"] == rxg.V_DISPATCH:
                 model.handle(int(r["tcb_idx"]), int(r["state"]), f)
+    # ip_in's learns: every TCP packet (all of the scenario's frames) from an unknown source
+    srcs = [int.from_bytes(f[26:30], "big") for f in frames]
+    known = sorted(set(srcs))[::2] if arp else []
+    exp_learn, seen = [], set(known)
+    for sip in srcs:
+        if sip not in seen:
+            seen.add(sip)
+            exp_learn.append(sip)
     # rxg: posts between bursts, handlers mirror inside them
     tcb, live = pktgen.table_arrays(rows)
     engine.tcb_load(tcb, live)
     engine.tcb_sync()
+    learned = []
+    if arp:
+        engine.arp_load(known)
+    else:
+        engine.arp_disable()
     gm = Model(list(rows), engine)
     bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
     addr = {C.addressof(b): i for i, b in enumerate(bufs)}
@@ -123,8 +139,13 @@ def test_random_bursts_equal_sequential_reference(engine, seed):
         gm.handle(idx, st, frames[i])
         return 0
 
+    def add_mac(u, ip, mac):
+        learned.append(ip)
+        return 1
+
     ops_t = rxg.HandoffOps(None, rxg.HANDOFF_FREE(free_mbuf), rxg.HANDOFF_ARP_IN(), rxg.HANDOFF_GET_MAC(),
-                           rxg.HANDOFF_ADD_MAC(), rxg.HANDOFF_SEND_RESET(rst), rxg.HANDOFF_ON_SEGMENT(),
+                           rxg.HANDOFF_ADD_MAC(add_mac) if arp else rxg.HANDOFF_ADD_MAC(),
+                           rxg.HANDOFF_SEND_RESET(rst), rxg.HANDOFF_ON_SEGMENT(),
                            rxg.HANDOFF_TCPSWITCH(tcpswitch))
     lib = rxg.load_library()
     for (b0, b1), ops in zip(cuts, plan):
@@ -142,6 +163,10 @@ def test_random_bursts_equal_sequential_reference(engine, seed):
         else:
             assert got[i] == ("free",), (i, got[i], exp[i])
     assert gm.rows == model.rows
+    if arp:
+        assert learned == exp_learn
+        assert engine.arp_count() == len(known) + len(exp_learn)
+        engine.arp_disable()
     # the device mirror ends as the reference's table
     t2, l2 = pktgen.table_arrays(model.rows)
     want, _ = oracle.rx_batch(*pktgen.pack_arena(frames[:500]), t2, l2)
