@@ -67,16 +67,21 @@ __device__ __forceinline__ Cand candidate(const PgArgs &a, uint32_t i)
 {
     Cand c{0ull, 0u, 0u};
     if (i >= a.n) return c;
+    // the record, the descriptor and the length are loaded together (one HBM round trip
+    // before the frame's header word, not two)
     // rxg_rec16: x tcb_idx | y checksums | z verdict, state<<8, tcp_flags<<16, flags<<24 | w datalen
     const uint4 r = *reinterpret_cast<const uint4 *>(a.recs + (size_t)i * a.stride);
+    const uint32_t off = a.off64[i];
+    const uint32_t flen = a.len[i];
+    asm volatile("" ::"v"(off), "v"(flen));  // keeps the two loads above the branch
     const uint32_t verdict = r.z & 0xFFu, rflags = r.z >> 24;
     const int32_t datalen = (int32_t)r.w;
     if (verdict > RXG_V_RST_LISTEN_NONSYN || datalen <= 0 || (rflags & RXG_F_TRUNC)) return c;
-    const uint64_t base = (uint64_t)a.off64[i] * 64u;
+    const uint64_t base = (uint64_t)off * 64u;
     // bytes 44..47 of the frame (>= 54 bytes: not RXG_F_TRUNC); data_off is byte 46
     const uint32_t dw = *reinterpret_cast<const uint32_t *>(a.frames + base + 44u);
     const uint32_t start = RXG_OFF_TCP + ((dw >> 20) & 0xFu) * 4u;
-    if (start + (uint32_t)datalen > (uint32_t)a.len[i]) return c;
+    if (start + (uint32_t)datalen > flen) return c;
     c.src = base + start;
     c.len = (uint32_t)datalen;
     // GetData asserts (Length - offset) < 1000, its stack buffer's size (tcp_windows.c:170)

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--variants", default="0", help="RXG_PG_VARIANT values, interleaved")
+    ap.add_argument("--check", action="store_true")
     args = ap.parse_args()
     engs = {}
     for v in args.variants.split(","):
@@ -38,7 +39,7 @@ def main():
         eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, recs.ptr, 16)
         lens = b["len"].download(np.uint16, n).astype(np.int64)
         pl = (lens - 54).clip(min=0)
-        cap = int(((pl + 15) // 16 * 16).sum())
+        cap = int(((pl + 127) // 128 * 128).sum())  # room for every alignment variant
         arena, msgs, used = eng.alloc(cap), eng.alloc(n * 16), eng.alloc(8)
         res = {v: [] for v in engs}
         for rnd in range(3):
@@ -54,6 +55,22 @@ def main():
                     e2.record(e)
                 e2.sync()
                 res[v] += [e2.elapsed_ms(a, e) for a, e in evs]
+        if args.check:
+            ref = None
+            for v, e2 in engs.items():
+                e2.payload_gather_dev(arena.ptr, cap, msgs.ptr, used.ptr)
+                e2.sync()
+                m = msgs.download(np.uint64, 2 * n).reshape(n, 2)
+                ar = arena.download(np.uint8, cap)
+                offs, ln = m[:, 0].astype(np.int64), (m[:, 1] & 0xFFFFFFFF).astype(np.int64)
+                u = int(used.download(np.uint64, 1)[0])
+                body = np.concatenate([ar[o:o + l] for o, l in zip(offs[:4096], ln[:4096])])
+                gaps = [ar[o + l:nxt] for o, l, nxt in zip(offs[:4095], ln[:4095], offs[1:4096]) if l]
+                zero = all((g == 0).all() for g in gaps)
+                if ref is None:
+                    ref = body
+                print(json.dumps({"variant": v, "workload": w, "used": u, "same_payload": bool(np.array_equal(body, ref)),
+                                  "pad_zero": bool(zero), "align": int(np.gcd.reduce(offs[ln > 0][:4096]))}), flush=True)
         alg = 2 * int(pl.sum()) + 32 * n
         for v, ms in res.items():
             ms = np.array(ms)
