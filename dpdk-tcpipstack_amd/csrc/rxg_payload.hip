@@ -16,7 +16,10 @@
 //              message descriptors, then each wave copies its 64 frames' payloads one
 //              16-byte destination chunk per lane (source misaligned by 54 mod 16 for a
 //              20-byte TCP header: 16-byte loads + a cross-lane byte funnel shift;
-//              destination 16-byte aligned, the tail of the last chunk zeroed).
+//              destination 16-byte aligned, the tail of the last chunk zeroed).  The
+//              copy's first two sets of rounds are loaded before the look-back (their
+//              sources and in-workgroup layout do not depend on it), so its latency
+//              overlaps them.
 //
 // A candidate is every TCP segment of the burst (verdict DISPATCH, RST_NOPCB or
 // RST_LISTEN_NONSYN: the replay may re-classify the latter two to a DISPATCH when a
@@ -279,6 +282,103 @@ __device__ __forceinline__ void copy_batch(const PgArgs &a, WaveCopy &W, uint64_
     __builtin_amdgcn_wave_barrier();  // W is rewritten by the next batch
 }
 
+// store_rounds for copy_batch_pre: the workgroup's arena base is known only after the
+// look-back, so W.dst holds offsets relative to it; payloads past the arena capacity were
+// loaded but are not stored (they get no message either)
+template <int kU, bool NT>
+__device__ __forceinline__ void store_rounds_at(const PgArgs &a, const WaveCopy &W, int lane, const Round (&R)[kU],
+                                                uint64_t base)
+{
+    const int nl = lane == 63 ? 63 : lane + 1;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint4 N0 = bperm16(R[u].A, nl);
+        const uint4 N = R[u].own ? R[u].E : N0;
+        const uint32_t L = W.len[R[u].p];
+        const uint64_t d = base + W.dst[R[u].p];
+        if (R[u].act && d + 16ull * ((L + 15u) >> 4) <= a.arena_cap) {
+            const uint64_t s = W.src[R[u].p];
+            const uint32_t sh = (uint32_t)(s & 15u);
+            uint4 o = sh ? funnel16(R[u].A, N, sh) : R[u].A;
+            const int vb = (int)L - (int)(16u * R[u].k);
+            if (vb < 16) {
+                o.x = keep_bytes(o.x, vb);
+                o.y = keep_bytes(o.y, vb - 4);
+                o.z = keep_bytes(o.z, vb - 8);
+                o.w = keep_bytes(o.w, vb - 12);
+            }
+            stp<NT>(a.arena + d + 16u * R[u].k, o);
+        }
+    }
+}
+
+// copy_batch with the first kU rounds' loads issued before the workgroup's arena offset is
+// known: `finish` runs the look-back (and the workgroup barrier every wave must reach) while
+// those loads are in flight, and returns the workgroup's arena base.  `rel`: this lane's
+// payload offset relative to that base.
+template <int kU, bool NT, int PRE, typename F>
+__device__ __forceinline__ void copy_batch_pre(const PgArgs &a, WaveCopy &W, uint64_t src, uint64_t rel, uint32_t L,
+                                               int lane, F finish)
+{
+    const bool valid = L != 0u;
+    const unsigned long long vm = __ballot(valid);
+    if (vm == 0ull) {
+        (void)finish();
+        return;
+    }
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
+    const uint32_t nch = valid ? (L + 15u) >> 4 : 0u;
+    const uint32_t incl = wave_incl_scan(nch, lane);
+    const uint32_t start = incl - nch;
+    const uint32_t T = (uint32_t)__shfl(incl, 63, 64);
+    if (valid) {
+        W.src[rank] = src;
+        W.dst[rank] = rel;
+        W.start[rank] = start;
+        W.len[rank] = L;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    constexpr uint32_t kStep = 64u * kU;
+    Round X[kU], Y[kU];
+    issue_rounds<kU, NT>(a, W, 0u, T, valid, start, lane, le, X);
+    if constexpr (PRE == 1) {
+        const uint64_t base = finish();
+        uint32_t r0 = 0;
+        for (;;) {
+            const bool more = r0 + kStep < T;
+            if (more) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, Y);
+            store_rounds_at<kU, NT>(a, W, lane, X, base);
+            if (!more) break;
+            r0 += kStep;
+            const bool more2 = r0 + kStep < T;
+            if (more2) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, X);
+            store_rounds_at<kU, NT>(a, W, lane, Y, base);
+            if (!more2) break;
+            r0 += kStep;
+        }
+    } else {
+        // both sets in flight across the look-back
+        bool haveY = kStep < T;
+        if (haveY) issue_rounds<kU, NT>(a, W, kStep, T, valid, start, lane, le, Y);
+        const uint64_t base = finish();
+        uint32_t r0 = 0;
+        for (;;) {
+            store_rounds_at<kU, NT>(a, W, lane, X, base);
+            if (!haveY) break;
+            r0 += kStep;
+            const bool more = r0 + kStep < T;
+            if (more) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, X);
+            store_rounds_at<kU, NT>(a, W, lane, Y, base);
+            if (!more) break;
+            r0 += kStep;
+            haveY = r0 + kStep < T;
+            if (haveY) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, Y);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();  // W is rewritten by the next batch
+}
+
 // status word flags
 constexpr uint32_t kAgg = 1u, kIncl = 2u;
 
@@ -342,7 +442,7 @@ __device__ __forceinline__ uint32_t look_back(const PgArgs &a, uint32_t vb, int 
 // FPT frames per thread (workgroup = 256 * FPT frames, thread t owns frames FPT*t ..
 // FPT*t + FPT-1 for the scan; wave w copies frames [64 FPT w, 64 FPT (w+1)) 64 at a time).
 // TICKET: virtual workgroup ids from an atomic ticket (dispatch-order independent).
-template <int kU, bool NT, int FPT, bool TICKET>
+template <int kU, bool NT, int FPT, bool TICKET, int PRE = 0>
 __global__ __launch_bounds__(kPgThreads) void pg_gather(PgArgs a)
 {
     constexpr int FPB = kPgThreads * FPT;
@@ -376,6 +476,43 @@ __global__ __launch_bounds__(kPgThreads) void pg_gather(PgArgs a)
     for (int k = 0; k < kPgThreads / 64; ++k) {
         agg += s_w[k];
         wex += k < w ? s_w[k] : 0u;
+    }
+    if constexpr (PRE != 0 && FPT == 1) {
+        // publish the aggregate, issue the first copy rounds, then look back (wave 0) while
+        // they are in flight
+        if (w == 0 && lane == 0)
+            __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, vb ? kAgg : kIncl, agg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t rel = ((uint64_t)wex + incl - mine) * 16ull;
+        auto finish = [&]() -> uint64_t {
+            if (w == 0) {
+                bool timed_out = false;
+                const uint32_t excl = vb ? look_back(a, vb, lane, timed_out) : 0u;
+                if (lane == 0) {
+                    if (vb)
+                        __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, kIncl, excl + agg),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (timed_out) atomicMax(a.used, ~0ull);
+                    else if (vb == a.nblocks - 1) atomicMax(a.used, (unsigned long long)(excl + agg) * 16ull);
+                    s_excl = excl;
+                }
+            }
+            __syncthreads();
+            const uint64_t base = (uint64_t)s_excl * 16ull;
+            const uint64_t off = base + rel;
+            const uint64_t r = 16ull * ((c[0].len + 15u) >> 4);
+            const bool fits = c[0].len != 0u && off + r <= a.arena_cap;
+            if (i0 < a.n) {
+                rxg_payload_msg m;
+                m.arena_off = fits ? off : 0ull;
+                m.len = fits ? c[0].len : 0u;
+                m.flags = fits ? c[0].flags : 0u;
+                a.msgs[i0] = m;
+            }
+            return base;
+        };
+        copy_batch_pre<kU, NT, PRE>(a, s_wc[w], c[0].src, rel, c[0].len, lane, finish);
+        return;
     }
     if (w == 0) {
         if (lane == 0)
@@ -461,7 +598,9 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     case 5: hipLaunchKernelGGL((pg_gather<4, true, 1, false>), g, b, 0, st, a); break;
     case 6: hipLaunchKernelGGL((pg_gather<4, true, 4, true>), g, b, 0, st, a); break;
     case 7: hipLaunchKernelGGL((pg_gather<4, true, 4, false>), g, b, 0, st, a); break;
-    default: hipLaunchKernelGGL((pg_gather<4, true, 1, true>), g, b, 0, st, a);
+    case 8: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 0>), g, b, 0, st, a); break;  // look-back first
+    case 9: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 1>), g, b, 0, st, a); break;  // one set early
+    default: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2>), g, b, 0, st, a);
     }
     *launched = (a.ticket && (P.variant != 5 && P.variant != 7)) ? a.nblocks : 0u;
     return hipGetLastError();
