@@ -54,6 +54,39 @@ def test_gather_rec48_and_arena_overflow(engine):
     assert 0 < (msgs["flags"] & opl.PM_GATHERED).sum() < 200
 
 
+def test_gather_arena_capacity_sweep(engine):
+    """Capacities at, just below and just above message boundaries (the copy is issued
+    before the workgroup's arena offset is known, so payloads past the capacity are loaded
+    and must not be stored, nor get a message)."""
+    rows, frames = pktgen.parity_set(6, 3000)
+    tcb, live = pktgen.table_arrays(rows)
+    arena, off, lens = pktgen.pack_arena(frames)
+    exp_recs, _ = oracle.rx_batch(arena, off, lens, tcb, live)
+    msgs, _, full = opl.gather(frames, exp_recs["c"], 1 << 40)
+    starts = np.sort(msgs["arena_off"][msgs["len"] > 0])
+    assert len(starts) > 500
+    caps = {16, full - 16, full}
+    for k in (1, len(starts) // 7, len(starts) // 2, len(starts) - 1):
+        b = int(starts[k])
+        caps |= {b - 1, b, b + 1, b + 16}
+    for cap in sorted(c for c in caps if 0 < c <= full):
+        m = check_gather(engine, frames, rows, cap=cap)
+        got = m["flags"] & opl.PM_GATHERED
+        assert (m["arena_off"][got > 0] + m["len"][got > 0] <= cap).all()
+        # nothing is written past the capacity: a guard of sentinel bytes after it
+        guard = 4096
+        da, dm, du = engine.alloc(cap + guard), engine.alloc(len(frames) * 16), engine.alloc(8)
+        try:
+            da.upload(np.full(cap + guard, 0xA5, dtype=np.uint8))
+            engine.payload_gather_dev(da.ptr, cap, dm.ptr, du.ptr)
+            engine.sync()
+            tail = da.download(np.uint8, guard, offset_bytes=cap)
+            assert (tail == 0xA5).all(), f"cap {cap}: the gather wrote past the arena capacity"
+        finally:
+            for d in (da, dm, du):
+                d.free()
+
+
 def test_gather_every_payload_length_and_offset(engine):
     """Each payload length 1..200 and 990..1010, data_off 5..15 (source alignment)."""
     dst = pktgen.ip4(192, 168, 78, 2)
