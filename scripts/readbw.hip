@@ -170,6 +170,21 @@ int main(int argc, char **argv)
         }
     }
     {
+        // C4's byte count (2^20 IMIX frames, mean 354.3 B = 371.5 MB) as one flat stream,
+        // rotating over 4 disjoint regions of buf (1.49 GB) so the MALL cannot hold it: an
+        // upper bound for any C4 access pattern at this launch size
+        const size_t n16_c4 = (size_t)371519488 / 16u;
+        int it = 0;
+        for (int g : {ncu * 3, ncu * 4, ncu * 8}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "c4_flat_nt_g%d", g);
+            timeit(nm, n16_c4 * 16.0, [&] {
+                const u32x4 *p = (const u32x4 *)buf + (size_t)(it++ % 4) * n16_c4;
+                flat<true, 4><<<g, 256>>>(p, n16_c4, out);
+            });
+        }
+    }
+    {
         // C2: 2^20 x 64 B frames per launch, 16 rotating copies (1 GiB)
         const unsigned n2 = 1u << 20;
         const int ncopy = 16;
