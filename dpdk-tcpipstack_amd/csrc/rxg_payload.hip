@@ -7,7 +7,7 @@
 // as 20 bytes whatever the IHL, like the parse).  rxg does that copy for a whole burst in
 // three launches:
 //
-//   pg_gather  ONE launch, 256 frames per workgroup: each workgroup sums its candidates'
+//   pg_gather  ONE launch, 512 frames per workgroup: each workgroup sums its candidates'
 //              arena space (each payload rounded up to 16 bytes so that every message starts
 //              16-byte aligned), finds its offset by a decoupled look-back over the
 //              workgroups before it (virtual workgroup ids from an atomic ticket, so every
@@ -35,7 +35,8 @@
 namespace rxg {
 namespace {
 
-constexpr int kPgThreads = 256;  // = frames per workgroup
+constexpr int kPgThreads = 256;  // frames per workgroup of the smallest form (status words are sized for it)
+constexpr int kPgThreadsProd = 512;  // production: 512 frames (8 waves) per workgroup
 constexpr int kMaxU = 4;         // copy rounds in flight per wave (max)
 constexpr uint32_t kSpinLimit = 1u << 22;
 
@@ -442,13 +443,13 @@ __device__ __forceinline__ uint32_t look_back(const PgArgs &a, uint32_t vb, int 
 // FPT frames per thread (workgroup = 256 * FPT frames, thread t owns frames FPT*t ..
 // FPT*t + FPT-1 for the scan; wave w copies frames [64 FPT w, 64 FPT (w+1)) 64 at a time).
 // TICKET: virtual workgroup ids from an atomic ticket (dispatch-order independent).
-template <int kU, bool NT, int FPT, bool TICKET, int PRE = 0>
-__global__ __launch_bounds__(kPgThreads) void pg_gather(PgArgs a)
+template <int kU, bool NT, int FPT, bool TICKET, int PRE = 0, int TPB = kPgThreads>
+__global__ __launch_bounds__(TPB) void pg_gather(PgArgs a)
 {
-    constexpr int FPB = kPgThreads * FPT;
+    constexpr int FPB = TPB * FPT;
     __shared__ uint32_t s_vb, s_excl;
-    __shared__ uint32_t s_w[kPgThreads / 64];
-    __shared__ WaveCopy s_wc[kPgThreads / 64];
+    __shared__ uint32_t s_w[TPB / 64];
+    __shared__ WaveCopy s_wc[TPB / 64];
     __shared__ uint64_t s_src[FPT > 1 ? FPB : 1];
     __shared__ uint64_t s_dst[FPT > 1 ? FPB : 1];
     __shared__ uint32_t s_len[FPT > 1 ? FPB : 1];
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(kPgThreads) void pg_gather(PgArgs a)
     __syncthreads();
     uint32_t agg = 0, wex = 0;
 #pragma unroll
-    for (int k = 0; k < kPgThreads / 64; ++k) {
+    for (int k = 0; k < TPB / 64; ++k) {
         agg += s_w[k];
         wex += k < w ? s_w[k] : 0u;
     }
@@ -591,8 +592,10 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     hipError_t e = hipMemsetAsync(P.used, 0, sizeof(unsigned long long), st);
     if (e != hipSuccess || P.n == 0) return e;
     const int fpt = (P.variant == 6 || P.variant == 7) ? 4 : 1;
-    a.nblocks = (P.n + kPgThreads * fpt - 1) / (kPgThreads * fpt);
-    const dim3 g(a.nblocks), b(kPgThreads);
+    // workgroup size of the kernel the switch below launches
+    const int tpb = (P.variant >= 1 && P.variant <= 10) ? kPgThreads : P.variant == 11 ? 1024 : kPgThreadsProd;
+    a.nblocks = (P.n + tpb * fpt - 1) / (tpb * fpt);
+    const dim3 g(a.nblocks), b(tpb);
     switch (P.variant) {  // experiment variants (RXG_PG_VARIANT); 0 = production
     case 1: hipLaunchKernelGGL((pg_gather<4, false, 1, true>), g, b, 0, st, a); break;
     case 5: hipLaunchKernelGGL((pg_gather<4, true, 1, false>), g, b, 0, st, a); break;
@@ -600,7 +603,9 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     case 7: hipLaunchKernelGGL((pg_gather<4, true, 4, false>), g, b, 0, st, a); break;
     case 8: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 0>), g, b, 0, st, a); break;  // look-back first
     case 9: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 1>), g, b, 0, st, a); break;  // one set early
-    default: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2>), g, b, 0, st, a);
+    case 10: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 256>), g, b, 0, st, a); break;
+    case 11: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 1024>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
     }
     *launched = (a.ticket && (P.variant != 5 && P.variant != 7)) ? a.nblocks : 0u;
     return hipGetLastError();
