@@ -127,6 +127,47 @@ def test_gather_c3_full_size_property(engine):
         d.free()
 
 
+def test_gather_c4_imix_full_size_property(engine):
+    """BASELINE C4 batch (2^20 IMIX frames 64/576/1500, 64 K flows; payloads of 10, 522 and
+    1 446 bytes mixed inside every workgroup): every payload gathered, messages packed in
+    packet order at 16-byte-rounded offsets, each message's bytes equal to the frame's
+    bytes 54..len and its padding zero."""
+    n, flows = 1 << 20, 65536
+    b = engine.synth(n=n, nflows=flows, mix=1, seed=0x5EED0004)
+    tcb, live = rxg.synthetic_tcb_table(flows)
+    engine.tcb_load(tcb, live)
+    engine.tcb_sync()
+    recs = engine.alloc(n * 16)
+    engine.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, recs.ptr, rxg.REC16)
+    lens = b["len"].download(np.uint16, n).astype(np.int64)
+    off = b["off64"].download(np.uint32, n).astype(np.int64) * 64
+    assert set(np.unique(lens)) == {64, 576, 1500}
+    pl = lens - 54
+    r16 = (pl + 15) // 16 * 16
+    cap = int(r16.sum())
+    arena, msgs, used = engine.alloc(cap), engine.alloc(n * 16), engine.alloc(8)
+    engine.payload_gather_dev(arena.ptr, cap, msgs.ptr, used.ptr)
+    engine.sync()
+    assert int(used.download(np.uint64, 1)[0]) == cap
+    m = msgs.download(rxg.PAYLOAD_MSG_DTYPE, n)
+    exp_off = np.concatenate([[0], np.cumsum(r16)[:-1]]).astype(np.uint64)
+    assert (m["len"] == pl).all() and (m["arena_off"] == exp_off).all()
+    assert ((m["flags"] & rxg.PM_GATHERED) != 0).all()
+    fr = b["arena"].download(np.uint8, b["arena_bytes"])
+    ga = arena.download(np.uint8, cap)
+    for L in (64, 576, 1500):  # one length class at a time, in chunks (host memory)
+        idx = np.nonzero(lens == L)[0]
+        P, R = L - 54, (L - 54 + 15) // 16 * 16
+        for c in range(0, len(idx), 1 << 15):
+            k = idx[c:c + (1 << 15)]
+            src = fr[(off[k] + 54)[:, None] + np.arange(P)]
+            dst = ga[exp_off[k].astype(np.int64)[:, None] + np.arange(R)]
+            assert np.array_equal(dst[:, :P], src), f"payload bytes differ (length {L})"
+            assert not dst[:, P:].any(), f"padding not zero (length {L})"
+    for d in (recs, arena, msgs, used):
+        d.free()
+
+
 # ------------------------------------------------------------------ end to end ---
 def multiflow_bursts(seed: int, nflows: int = 40, nseg: int = 10):
     """Clients connect, stream segments (some reordered, duplicated, or ending right at the
