@@ -7,7 +7,7 @@
 // as 20 bytes whatever the IHL, like the parse).  rxg does that copy for a whole burst in
 // three launches:
 //
-//   pg_gather  ONE launch, 512 frames per workgroup: each workgroup sums its candidates'
+//   pg_gather  ONE launch, 1 024 frames per workgroup: each workgroup sums its candidates'
 //              arena space (each payload rounded up to 16 bytes so that every message starts
 //              16-byte aligned), finds its offset by a decoupled look-back over the
 //              workgroups before it (virtual workgroup ids from an atomic ticket, so every
@@ -36,7 +36,10 @@ namespace rxg {
 namespace {
 
 constexpr int kPgThreads = 256;  // frames per workgroup of the smallest form (status words are sized for it)
-constexpr int kPgThreadsProd = 512;  // production: 512 frames (8 waves) per workgroup
+// production: 1 024 frames (16 waves) per workgroup, 2 copy rounds per set (80 VGPRs,
+// 6 waves per SIMD), DESIGN.md §5
+constexpr int kPgThreadsProd = 1024;
+constexpr int kPgRoundsProd = 2;
 constexpr int kMaxU = 4;         // copy rounds in flight per wave (max)
 constexpr uint32_t kSpinLimit = 1u << 22;
 
@@ -593,7 +596,7 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     if (e != hipSuccess || P.n == 0) return e;
     const int fpt = (P.variant == 6 || P.variant == 7) ? 4 : 1;
     // workgroup size of the kernel the switch below launches
-    const int tpb = (P.variant >= 1 && P.variant <= 10) ? kPgThreads : P.variant == 11 ? 1024 : kPgThreadsProd;
+    const int tpb = (P.variant >= 1 && P.variant <= 10) ? kPgThreads : P.variant == 12 ? 512 : kPgThreadsProd;
     a.nblocks = (P.n + tpb * fpt - 1) / (tpb * fpt);
     const dim3 g(a.nblocks), b(tpb);
     switch (P.variant) {  // experiment variants (RXG_PG_VARIANT); 0 = production
@@ -605,7 +608,8 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     case 9: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 1>), g, b, 0, st, a); break;  // one set early
     case 10: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 256>), g, b, 0, st, a); break;
     case 11: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 1024>), g, b, 0, st, a); break;
-    default: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
+    case 12: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 512>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
     }
     *launched = (a.ticket && (P.variant != 5 && P.variant != 7)) ? a.nblocks : 0u;
     return hipGetLastError();
