@@ -1,5 +1,6 @@
 // rxg_common.h — definitions shared by rxg's host code and its gfx950 kernels.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "rxg.h"

@@ -92,7 +92,7 @@ extern "C" int rxg_group_init(const int32_t *devices, uint32_t ndev, const rxg_c
     *out = nullptr;
     rxg_group *g = new rxg_group();
     for (uint32_t i = 0; i < ndev; ++i) {
-        rxg_config c = cfg ? *cfg : rxg_config{0, 0, 0, 0};
+        rxg_config c = cfg ? *cfg : rxg_config{};
         c.device = devices[i];
         rxg_ctx *ctx = nullptr;
         const int rc = rxg_init(&c, &ctx);
@@ -256,6 +256,9 @@ extern "C" int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, voi
     so.send_reset = ops->send_reset ? sh_rst : nullptr;
     so.on_segment = ops->on_segment ? sh_seg : nullptr;
     so.tcpswitch = ops->tcpswitch ? sh_switch : nullptr;
+    so.tcpnopcb = ops->tcpnopcb;  // the caller's globals, bumped in packet order across shards
+    so.tcpchecksumerror = ops->tcpchecksumerror;
+    so.flags = ops->flags;
     struct Guard {
         rxg_group *g;
         ~Guard() { g->replaying = -1; }

@@ -20,6 +20,7 @@
 #include "rxg.h"
 #include "rxg_common.h"
 #include "rxg_kernels.h"
+#include "rxg_mirror.h"
 #include "rxg_opqueue.h"
 
 using namespace rxg;
@@ -59,25 +60,37 @@ struct DevBuf {
 struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    uint32_t max_blocks = 2048;     // RXG_MAX_BLOCKS overrides the occupancy-derived grid
+    uint32_t max_blocks = 0;        // rxg_config.max_blocks: grid cap (0 = occupancy grid)
     uint32_t grid_rec16 = 0, grid_rec48 = 0, grid_tx = 0;
-    int variant = 0;  // RXG_VARIANT: experiment kernels (tools/kbench only)
-    int nocount = 0;  // RXG_NOCOUNT: experiment only, skip the counter reduction
-    int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather experiment kernels
+    // Experiment switches: only an experiment build (make experiments, -DRXG_EXPERIMENTS,
+    // rxg/librxg_exp.so for scripts/kbench.py and pgbench.py) reads them from the
+    // environment; in the product library they stay 0.
+    int variant = 0;     // RXG_VARIANT: rx kernel variants (class subsets, ablations)
+    int nocount = 0;     // RXG_NOCOUNT: skip the counter reduction
+    int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather variants
 
     // tcbs[] writes posted by other threads (rxg_tcb_post), applied by the rx thread
     rxg::MpscRing<rxg_tcb_op> posted{RXG_TCB_QUEUE_CAP};
 
-    // host mirror of tcbs[0..ntcb)
-    std::vector<rxg_tcb_tuple> tcb;
-    std::vector<uint8_t> live;
-    bool dirty = true;
+    // host mirror of tcbs[0..ntcb) and the device words each write changes (rxg_mirror.h)
+    TcbMirror mir;
+    bool dirty = true;  // mirror writes not on the device yet
 
     // device mirror
     DevBuf buckets, listen;
     uint32_t bucket_mask = 0;
     int32_t dev_ntcb = 0;
     int32_t dev_min_null = INT32_MAX;
+    // Ordering of table writes against the kernels that read the tables:
+    // mirror writes run on `stream`; a burst on another stream waits for mirror_ev, and the
+    // next mirror write waits for read_ev, recorded after a table-reading launch on a
+    // stream other than `stream`.
+    hipEvent_t mirror_ev = nullptr, read_ev = nullptr;
+    bool mirror_ev_set = false, read_ev_set = false;
+    MirrorPatch *h_patch = nullptr;  // pinned: the patch kernel reads it over PCIe
+    uint32_t h_patch_cap = 0;
+    hipEvent_t patch_ev = nullptr;   // the last patch kernel (h_patch is free after it)
+    bool patch_ev_set = false;
 
     unsigned long long *counters = nullptr;
 
@@ -111,13 +124,19 @@ struct rxg_ctx {
     hipEvent_t pm_ev = nullptr;
     int64_t replay_pos = -1;  // packet whose handlers rxg_rx_replay is running
 
-    // ARP mirror (host set + device open-addressing table)
+    // ARP mirror (host set + device open-addressing table, rxg_mirror.h)
     bool arp_enabled = false, arp_dirty = false;
-    std::vector<uint32_t> arp_ips;              // in add_mac order
-    std::unordered_map<uint32_t, int> arp_set;
+    ArpMirror arp;
     std::unordered_map<uint32_t, int> arp_since_burst;  // learned after the last burst
     DevBuf d_arp;
     uint32_t arp_mask = 0;
+
+    // replay scratch, kept across calls (no per-burst allocation of the dport map)
+    std::vector<uint8_t> rp_hit = std::vector<uint8_t>(65536, 0);
+    std::vector<rxg_rec16> rp_cur;
+    std::vector<uint8_t> rp_stale;
+    const uint64_t *pm_used = nullptr;  // the gather's arena_used (device)
+    bool pm_poisoned = false;           // that gather timed out: no payload is handed out
 
     // host-buffer burst staging
     uint32_t max_batch = 0;
@@ -157,7 +176,11 @@ extern "C" int rxg_abi_version(void) { return RXG_ABI_VERSION; }
 
 extern "C" const char *rxg_build_info(void)
 {
+#ifdef RXG_EXPERIMENTS
+    return "rxg " __DATE__ " gfx950 experiments";
+#else
     return "rxg " __DATE__ " gfx950";
+#endif
 }
 
 extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
@@ -183,16 +206,27 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
         c->grid_rec16 = cus * (uint32_t)rx_blocks_per_cu(16);
         c->grid_rec48 = cus * (uint32_t)rx_blocks_per_cu(48);
         c->grid_tx = cus * (uint32_t)rx_blocks_per_cu(0);
-        c->max_blocks = 0;
-        if (const char *g = getenv("RXG_MAX_BLOCKS")) c->max_blocks = (uint32_t)atoi(g);
     }
+    if (cfg) {
+        c->max_blocks = cfg->max_blocks;
+        if (cfg->zc_bytes) c->zc_bytes = cfg->zc_bytes;
+    }
+#ifdef RXG_EXPERIMENTS
+    if (const char *g = getenv("RXG_MAX_BLOCKS")) c->max_blocks = (uint32_t)atoi(g);
     if (const char *v = getenv("RXG_VARIANT")) c->variant = atoi(v);
     if (const char *v = getenv("RXG_NOCOUNT")) c->nocount = atoi(v);
     if (const char *v = getenv("RXG_PG_VARIANT")) c->pg_variant = atoi(v);
     if (const char *v = getenv("RXG_ZC_BYTES")) c->zc_bytes = strtoull(v, nullptr, 10);
+#endif
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(-EIO, "rxg_init: hipStreamCreate failed");
+    }
+    if (hipEventCreateWithFlags(&c->mirror_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->read_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->patch_ev, hipEventDisableTiming) != hipSuccess) {
+        rxg_fini(c);
+        return fail(-EIO, "rxg_init: hipEventCreate failed");
     }
     if (hipMalloc(&c->counters, kCounterBytes) != hipSuccess ||
         hipMemset(c->counters, 0, kCounterBytes) != hipSuccess) {
@@ -230,6 +264,9 @@ extern "C" int rxg_fini(rxg_ctx *c)
         if (b->p) (void)hipFree(b->p);
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
+    if (c->h_patch) (void)hipHostFree(c->h_patch);
+    for (hipEvent_t e : {c->mirror_ev, c->read_ev, c->patch_ev})
+        if (e) (void)hipEventDestroy(e);
     if (c->counters) (void)hipFree(c->counters);
     if (c->h_arena) (void)hipHostFree(c->h_arena);
     if (c->h_off) (void)hipHostFree(c->h_off);
@@ -256,28 +293,18 @@ extern "C" void *rxg_stream(rxg_ctx *c) { return c ? (void *)c->stream : nullptr
 static hipStream_t pick(rxg_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
 
 // -------------------------------------------------------------------- TCB mirror ---
-static int grow_to(rxg_ctx *c, int32_t idx)
-{
-    if (idx < 0 || idx >= kMaxTcbs) return fail(-EINVAL, "tcb index %d outside 0..%d", idx, kMaxTcbs - 1);
-    if ((size_t)idx >= c->tcb.size()) {
-        c->tcb.resize((size_t)idx + 1, rxg_tcb_tuple{});
-        c->live.resize((size_t)idx + 1, 0);
-    }
-    return 0;
-}
-
 extern "C" int rxg_tcb_upsert(rxg_ctx *c, int32_t idx, const rxg_tcb_tuple *t)
 {
     if (!c || !t) return fail(-EINVAL, "rxg_tcb_upsert: NULL argument");
     if (t->state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_upsert: state %u", t->state);
-    const size_t old_n = c->tcb.size();
-    int rc = grow_to(c, idx);
-    if (rc) return rc;
-    if ((size_t)idx > old_n) c->touched_pass2 = true;  // slots old_n..idx-1 appear as NULL
-    if ((size_t)idx < old_n && c->live[idx]) c->touched.push_back(c->tcb[idx].dport);
+    if (idx < 0 || idx >= kMaxTcbs) return fail(-EINVAL, "tcb index %d outside 0..%d", idx, kMaxTcbs - 1);
+    const int32_t old_n = c->mir.ntcb();
+    // a NULL slot appears (slots old_n..idx-1) or disappears (a removed slot reused): the
+    // pass-2 NULL flag of later packets can change
+    if (idx > old_n || (idx < old_n && !c->mir.live[idx])) c->touched_pass2 = true;
+    if (idx < old_n && c->mir.live[idx]) c->touched.push_back(c->mir.tcb[idx].dport);
     c->touched.push_back(t->dport);
-    c->tcb[idx] = *t;
-    c->live[idx] = 1;
+    c->mir.upsert(idx, *t);
     c->dirty = true;
     c->gen++;
     return 0;
@@ -286,11 +313,11 @@ extern "C" int rxg_tcb_upsert(rxg_ctx *c, int32_t idx, const rxg_tcb_tuple *t)
 extern "C" int rxg_tcb_remove(rxg_ctx *c, int32_t idx)
 {
     if (!c) return fail(-EINVAL, "rxg_tcb_remove: ctx NULL");
-    if (idx < 0 || (size_t)idx >= c->tcb.size())
-        return fail(-EINVAL, "rxg_tcb_remove: index %d outside Ntcb %zu", idx, c->tcb.size());
-    if (c->live[idx]) c->touched.push_back(c->tcb[idx].dport);
+    if (idx < 0 || idx >= c->mir.ntcb())
+        return fail(-EINVAL, "rxg_tcb_remove: index %d outside Ntcb %d", idx, c->mir.ntcb());
+    if (c->mir.live[idx]) c->touched.push_back(c->mir.tcb[idx].dport);
     c->touched_pass2 = true;
-    c->live[idx] = 0;
+    c->mir.remove(idx);
     if ((size_t)idx < c->rcv_state.size()) c->rcv_state[idx] = 0;  // FreeWindow
     c->dirty = true;
     c->gen++;
@@ -301,10 +328,10 @@ extern "C" int rxg_tcb_set_state(rxg_ctx *c, int32_t idx, uint8_t state)
 {
     if (!c) return fail(-EINVAL, "rxg_tcb_set_state: ctx NULL");
     if (state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_set_state: state %u", state);
-    if (idx < 0 || (size_t)idx >= c->tcb.size() || !c->live[idx])
+    if (idx < 0 || idx >= c->mir.ntcb() || !c->mir.live[idx])
         return fail(-EINVAL, "rxg_tcb_set_state: index %d is not a live slot", idx);
-    c->touched.push_back(c->tcb[idx].dport);
-    c->tcb[idx].state = state;
+    c->touched.push_back(c->mir.tcb[idx].dport);
+    c->mir.set_state(idx, state);
     c->dirty = true;
     c->gen++;
     return 0;
@@ -317,11 +344,7 @@ extern "C" int rxg_tcb_load(rxg_ctx *c, const rxg_tcb_tuple *tcbs, const uint8_t
     for (int32_t i = 0; i < ntcb; ++i)
         if ((!live || live[i]) && tcbs[i].state >= RXG_TCP_STATES)
             return fail(-EINVAL, "rxg_tcb_load: slot %d state %u", i, tcbs[i].state);
-    c->tcb.assign(tcbs, tcbs + ntcb);
-    if (live)
-        c->live.assign(live, live + ntcb);
-    else
-        c->live.assign((size_t)ntcb, 1);
+    c->mir.load(tcbs, live, ntcb);
     c->dirty = true;
     c->touched_all = true;
     c->gen++;
@@ -330,11 +353,8 @@ extern "C" int rxg_tcb_load(rxg_ctx *c, const rxg_tcb_tuple *tcbs, const uint8_t
     return 0;
 }
 
-extern "C" int32_t rxg_tcb_count(rxg_ctx *c) { return c ? (int32_t)c->tcb.size() : -EINVAL; }
+extern "C" int32_t rxg_tcb_count(rxg_ctx *c) { return c ? c->mir.ntcb() : -EINVAL; }
 
-static inline bool port_ok(int32_t p) { return p >= 0 && p <= 0xFFFF; }
-
-// Rebuild the device mirror from the host mirror (DESIGN.md §TCB mirror).
 extern "C" int rxg_tcb_post(rxg_ctx *c, const rxg_tcb_op *op)
 {
     if (!c || !op) return fail(-EINVAL, "rxg_tcb_post: NULL argument");
@@ -371,72 +391,74 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
     return c->dirty ? tcb_push(c) : 0;
 }
 
-// Rebuild the device mirror from the host mirror (no draining: inside a replay only the rx
-// thread's own writes count, sequentially).
+// Before a mirror write on c->stream: kernels that read the tables on another stream are done.
+static int wait_table_readers(rxg_ctx *c)
+{
+    if (c->read_ev_set) {
+        HIP_OK(hipStreamWaitEvent(c->stream, c->read_ev, 0));
+        c->read_ev_set = false;
+    }
+    return 0;
+}
+
+// The patches of the TCB and ARP mirrors, in one launch on c->stream.
+static int apply_patches(rxg_ctx *c, std::vector<MirrorPatch> &p)
+{
+    dedupe_patches(p);
+    if (p.empty()) return 0;
+    if (c->patch_ev_set) HIP_OK(hipEventSynchronize(c->patch_ev));  // h_patch free again
+    if (p.size() > c->h_patch_cap) {
+        if (c->h_patch) HIP_OK(hipHostFree(c->h_patch));
+        c->h_patch = nullptr;
+        c->h_patch_cap = 0;
+        const uint32_t cap = (uint32_t)std::max<size_t>(p.size() * 2, 1024);
+        HIP_OK(hipHostMalloc((void **)&c->h_patch, (size_t)cap * sizeof(MirrorPatch), hipHostMallocDefault));
+        c->h_patch_cap = cap;
+    }
+    std::memcpy(c->h_patch, p.data(), p.size() * sizeof(MirrorPatch));
+    int rc = wait_table_readers(c);
+    if (rc) return rc;
+    HIP_OK(launch_mirror_patch(c->h_patch, (uint32_t)p.size(), (uint4 *)c->buckets.p, (int32_t *)c->listen.p,
+                               (uint2 *)c->d_arp.p, c->stream));
+    HIP_OK(hipEventRecord(c->patch_ev, c->stream));
+    c->patch_ev_set = true;
+    HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
+    c->mirror_ev_set = true;
+    p.clear();
+    return 0;
+}
+
+// Bring the device TCB mirror up to date: the changed words (usual) or, after a load or
+// past load 1/2, the whole table.  No host block on the patch path.
 static int tcb_push(rxg_ctx *c)
 {
     if (!c->dirty) return 0;
     int rc = set_device(c);
     if (rc) return rc;
-    const int32_t n = (int32_t)c->tcb.size();
-
-    // exact tuples -> lowest index (pass 1 returns the first live match)
-    struct Key {
-        uint32_t ports, dst, src;
-        bool operator==(const Key &o) const { return ports == o.ports && dst == o.dst && src == o.src; }
-    };
-    struct KeyHash {
-        size_t operator()(const Key &k) const { return tuple_hash(k.ports, k.dst, k.src); }
-    };
-    std::unordered_map<Key, int32_t, KeyHash> first;
-    first.reserve((size_t)n * 2 + 1);
-    std::vector<int32_t> listen(65536, -1);
-    int32_t min_null = INT32_MAX;
-    for (int32_t i = 0; i < n; ++i) {
-        if (!c->live[i]) {
-            if (min_null == INT32_MAX) min_null = i;
-            continue;
+    TcbMirror &m = c->mir;
+    if (m.need_rebuild) {
+        m.rebuild();
+        const size_t sb = m.slots.size() * sizeof(Slot), lb = m.listen.size() * sizeof(int32_t);
+        if (sb > c->buckets.bytes || lb > c->listen.bytes) {
+            // the old buffers must be idle before they are freed
+            if (c->read_ev_set) HIP_OK(hipEventSynchronize(c->read_ev));
+            HIP_OK(hipStreamSynchronize(c->stream));
+            if ((rc = ensure(c->buckets, sb))) return rc;
+            if ((rc = ensure(c->listen, lb))) return rc;
         }
-        const rxg_tcb_tuple &t = c->tcb[i];
-        // a tuple whose int ports are outside 0..65535 can never equal a packet's u16 port
-        if (port_ok(t.dport) && port_ok(t.sport)) {
-            Key k{((uint32_t)t.dport << 16) | (uint32_t)t.sport, t.ipv4_dst, t.ipv4_src};
-            first.emplace(k, i);  // keeps the lowest index
-        }
-        if (t.state == RXG_LISTENING && port_ok(t.dport) && listen[t.dport] < 0) listen[t.dport] = i;
+        if ((rc = wait_table_readers(c))) return rc;
+        HIP_OK(hipMemcpyAsync(c->buckets.p, m.slots.data(), sb, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(c->listen.p, m.listen.data(), lb, hipMemcpyHostToDevice, c->stream));
+        // the next write changes m.slots in place: the copies must have consumed them
+        HIP_OK(hipStreamSynchronize(c->stream));
+        HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
+        c->mirror_ev_set = true;
+    } else if ((rc = apply_patches(c, m.patches))) {
+        return rc;
     }
-    // buckets: load factor <= 1/2 of the slots
-    uint32_t nb = 1;
-    while ((uint64_t)nb * kSlotsPerBucket < (uint64_t)first.size() * 2u) nb <<= 1;
-    std::vector<uint32_t> slots((size_t)nb * kSlotsPerBucket * 4u, 0u);
-    for (size_t s = 0; s < (size_t)nb * kSlotsPerBucket; ++s) slots[s * 4 + 3] = kEmpty;
-    for (const auto &kv : first) {
-        uint32_t b = tuple_hash(kv.first.ports, kv.first.dst, kv.first.src) & (nb - 1);
-        for (;;) {
-            int placed = 0;
-            for (int s = 0; s < kSlotsPerBucket && !placed; ++s) {
-                uint32_t *e = &slots[((size_t)b * kSlotsPerBucket + s) * 4];
-                if (e[3] == kEmpty) {
-                    e[0] = kv.first.ports;
-                    e[1] = kv.first.dst;
-                    e[2] = kv.first.src;
-                    e[3] = (uint32_t)kv.second | ((uint32_t)c->tcb[kv.second].state << kStateShift);
-                    placed = 1;
-                }
-            }
-            if (placed) break;
-            b = (b + 1) & (nb - 1);
-        }
-    }
-    if ((rc = ensure(c->buckets, slots.size() * 4))) return rc;
-    if ((rc = ensure(c->listen, listen.size() * 4))) return rc;
-    HIP_OK(hipMemcpyAsync(c->buckets.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(c->listen.p, listen.data(), listen.size() * 4, hipMemcpyHostToDevice, c->stream));
-    // the host vectors die here: the copies must have consumed them
-    HIP_OK(hipStreamSynchronize(c->stream));
-    c->bucket_mask = nb - 1;
-    c->dev_ntcb = n;
-    c->dev_min_null = min_null;
+    c->bucket_mask = m.nb - 1;
+    c->dev_ntcb = m.ntcb();
+    c->dev_min_null = m.min_null;
     c->dirty = false;
     return 0;
 }
@@ -446,10 +468,7 @@ extern "C" int rxg_arp_learned(rxg_ctx *c, uint32_t ip)
 {
     if (!c) return fail(-EINVAL, "rxg_arp_learned: ctx NULL");
     c->arp_enabled = true;
-    if (c->arp_set.emplace(ip, 1).second) {
-        c->arp_ips.push_back(ip);
-        c->arp_dirty = true;
-    }
+    if (c->arp.add(ip)) c->arp_dirty = true;
     c->arp_since_burst.emplace(ip, 1);
     return 0;
 }
@@ -458,44 +477,64 @@ extern "C" int rxg_arp_load(rxg_ctx *c, const uint32_t *ips, uint32_t n)
 {
     if (!c || (n && !ips)) return fail(-EINVAL, "rxg_arp_load: bad arguments");
     c->arp_enabled = true;
-    c->arp_ips.clear();
-    c->arp_set.clear();
-    for (uint32_t i = 0; i < n; ++i)
-        if (c->arp_set.emplace(ips[i], 1).second) c->arp_ips.push_back(ips[i]);
+    c->arp.clear();
+    for (uint32_t i = 0; i < n; ++i) c->arp.add(ips[i]);
     c->arp_dirty = true;
     return 0;
 }
 
-extern "C" int32_t rxg_arp_count(rxg_ctx *c) { return c ? (int32_t)c->arp_ips.size() : -EINVAL; }
+extern "C" int32_t rxg_arp_count(rxg_ctx *c) { return c ? (int32_t)c->arp.ips.size() : -EINVAL; }
 
 extern "C" int rxg_arp_disable(rxg_ctx *c)
 {
     if (!c) return fail(-EINVAL, "rxg_arp_disable: ctx NULL");
     c->arp_enabled = false;
-    c->arp_ips.clear();
-    c->arp_set.clear();
+    c->arp.clear();
     c->arp_since_burst.clear();
+    c->arp_dirty = true;
     return 0;
 }
 
 static int arp_sync(rxg_ctx *c)
 {
     if (!c->arp_enabled || !c->arp_dirty) return 0;
-    uint32_t ns = 16;
-    while ((uint64_t)ns < (uint64_t)c->arp_ips.size() * 2u) ns <<= 1;
-    std::vector<uint32_t> slots((size_t)ns * 2u, 0u);
-    for (uint32_t ip : c->arp_ips) {
-        uint32_t h = arp_hash(ip) & (ns - 1);
-        while (slots[(size_t)h * 2 + 1]) h = (h + 1) & (ns - 1);
-        slots[(size_t)h * 2] = ip;
-        slots[(size_t)h * 2 + 1] = 1;
+    ArpMirror &a = c->arp;
+    int rc;
+    if (a.need_rebuild) {
+        a.rebuild();
+        const size_t bytes = a.slots.size() * 4;
+        if (bytes > c->d_arp.bytes) {
+            if (c->read_ev_set) HIP_OK(hipEventSynchronize(c->read_ev));
+            HIP_OK(hipStreamSynchronize(c->stream));
+            if ((rc = ensure(c->d_arp, bytes))) return rc;
+        }
+        if ((rc = wait_table_readers(c))) return rc;
+        HIP_OK(hipMemcpyAsync(c->d_arp.p, a.slots.data(), bytes, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
+        c->mirror_ev_set = true;
+    } else if ((rc = apply_patches(c, a.patches))) {
+        return rc;
     }
-    int rc = ensure(c->d_arp, slots.size() * 4);
-    if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(c->d_arp.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
-    c->arp_mask = ns - 1;
+    c->arp_mask = a.ns - 1;
     c->arp_dirty = false;
+    return 0;
+}
+
+// A launch on `st` that reads the mirror tables: it follows the last mirror write, and
+// the next mirror write follows it.
+static int order_table_reader_before(rxg_ctx *c, hipStream_t st)
+{
+    if (st != c->stream && c->mirror_ev_set) HIP_OK(hipStreamWaitEvent(st, c->mirror_ev, 0));
+    return 0;
+}
+
+static int order_table_reader_after(rxg_ctx *c, hipStream_t st)
+{
+    if (st != c->stream) {
+        HIP_OK(hipEventRecord(c->read_ev, st));
+        c->read_ev_set = true;
+    }
     return 0;
 }
 
@@ -550,7 +589,10 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
     L.max_blocks = c->max_blocks ? c->max_blocks : (b->rec_kind == RXG_REC48 ? c->grid_rec48 : c->grid_rec16);
     if (L.max_blocks == 0) L.max_blocks = 1024;
     L.variant = c->variant;
-    HIP_OK(launch_rx(L, pick(c, stream)));
+    hipStream_t st = pick(c, stream);
+    if ((rc = order_table_reader_before(c, st))) return rc;
+    HIP_OK(launch_rx(L, st));
+    if ((rc = order_table_reader_after(c, st))) return rc;
     c->burst_ok = true;
     return 0;
 }
@@ -695,6 +737,9 @@ extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void
         HIP_OK(hipMemsetAsync(c->d_pg_ticket.p, 0, sizeof(unsigned long long), st));
         c->pg_tickets = 0;
     }
+    // one gather in flight per context: the ticket counter and the status words are shared,
+    // so a gather on another stream waits for the previous one
+    if (c->pm_ev) HIP_OK(hipStreamWaitEvent(st, c->pm_ev, 0));
     c->pg_epoch = (c->pg_epoch % ((1u << 30) - 1u)) + 1u;
     LaunchPayload P;
     P.frames = c->last_frames;
@@ -719,8 +764,10 @@ extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void
     if (!c->pm_ev) HIP_OK(hipEventCreateWithFlags(&c->pm_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(c->pm_ev, st));
     c->d_pm = o->msgs;
+    c->pm_used = o->arena_used;
     c->pm_n = n;
     c->pm_pending = true;
+    c->pm_poisoned = false;
     return 0;
 }
 
@@ -757,11 +804,17 @@ extern "C" int rxg_payload_take(rxg_ctx *c, int32_t idx, uint32_t seq, uint32_t 
             HIP_OK(hipHostMalloc((void **)&c->h_pm, (size_t)c->pm_n * sizeof(rxg_payload_msg), hipHostMallocDefault));
             c->h_pm_cap = c->pm_n;
         }
+        uint64_t used = 0;
         HIP_OK(hipMemcpyAsync(c->h_pm, c->d_pm, (size_t)c->pm_n * sizeof(rxg_payload_msg), hipMemcpyDeviceToHost,
                               c->stream));
+        HIP_OK(hipMemcpyAsync(&used, c->pm_used, sizeof used, hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
         c->pm_pending = false;
+        // a gather whose look-back timed out (arena_used = ~0) placed payloads at unknown
+        // offsets: nothing of that burst is handed out (the stack's own PushData runs)
+        c->pm_poisoned = used == ~0ull;
     }
+    if (c->pm_poisoned) return 0;
     const rxg_payload_msg &m = c->h_pm[pos];
     if (!(m.flags & RXG_PM_GATHERED) || m.len != length) return 0;
     if (idx < 0 || (size_t)idx >= c->rcv_state.size() || c->rcv_state[idx] != 1 || c->rcv_cur[idx] != seq)
@@ -838,7 +891,7 @@ static int reclassify(rxg_ctx *c, const std::vector<uint32_t> &sel, std::vector<
     L.out = (uint8_t *)c->d_fix.p;
     L.table = table_view(c);
     L.counters = nullptr;  // corrections go to the host row instead
-    L.max_blocks = c->grid_rec16 ? c->grid_rec16 : 1024;
+    L.max_blocks = c->max_blocks ? c->max_blocks : (c->grid_rec16 ? c->grid_rec16 : 1024);
     HIP_OK(launch_rx(L, c->stream));
     out.resize(sel.size());
     HIP_OK(hipMemcpyAsync(out.data(), c->d_fix.p, sel.size() * sizeof(rxg_rec16), hipMemcpyDeviceToHost, c->stream));
@@ -862,11 +915,13 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         rxg_ctx *c;
         ~PosGuard() { c->replay_pos = -1; }
     } pos_guard{c};
-    std::vector<rxg_rec16> cur(n);
+    std::vector<rxg_rec16> &cur = c->rp_cur;
+    cur.resize(n);
     for (uint32_t i = 0; i < n; ++i) cur[i] = *(const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
-    std::vector<uint8_t> stale(n, 0);
+    std::vector<uint8_t> &stale = c->rp_stale;
+    stale.assign(n, 0);
     int64_t delta[RXG_NCOUNTERS] = {0};
-    std::vector<uint8_t> hit(65536, 0);
+    std::vector<uint8_t> &hit = c->rp_hit;  // all zero between uses
     // Mark the TCP packets j >= j0 whose classification the tracked changes can affect,
     // then forget the changes.  The dport is re-read from the frame (>= 54 bytes unless
     // RXG_F_TRUNC, which is marked conservatively).
@@ -935,7 +990,12 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
                 if (ops->get_mac && ops->add_mac && ops->get_mac(ops->user, src, mac) == 0)
                     ops->add_mac(ops->user, src, f + 6);
             }
-            if (r.verdict == RXG_V_RST_NOPCB || r.verdict == RXG_V_RST_LISTEN_NONSYN) {
+            if ((ops->flags & RXG_OPS_VERIFY_TCP_CKSUM) && !(r.flags & RXG_F_TCP_OK)) {
+                // tcp_in.c:37-40 with the check compiled in: free, ++tcpchecksumerror
+                if (ops->free_mbuf) ops->free_mbuf(ops->user, m);
+                if (ops->tcpchecksumerror) ++*ops->tcpchecksumerror;
+            } else if (r.verdict == RXG_V_RST_NOPCB || r.verdict == RXG_V_RST_LISTEN_NONSYN) {
+                if (r.verdict == RXG_V_RST_NOPCB && ops->tcpnopcb) ++*ops->tcpnopcb;  // tcp_in.c:48
                 if (ops->free_mbuf) ops->free_mbuf(ops->user, m);
                 if (ops->send_reset) ops->send_reset(ops->user, ip, tcp);
             } else {  // RXG_V_DISPATCH

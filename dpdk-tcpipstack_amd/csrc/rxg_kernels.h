@@ -55,5 +55,9 @@ uint32_t payload_blocks(uint32_t n);
 // resident 256-thread workgroups per CU of the production kernel of `mode`
 int rx_blocks_per_cu(int mode);
 hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);
+// rxg_mirror.h patches (n of them, host-visible memory) applied to the device mirror tables
+struct MirrorPatch;
+hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets, int32_t *listen, uint2 *arp,
+                               hipStream_t st);
 
 }  // namespace rxg

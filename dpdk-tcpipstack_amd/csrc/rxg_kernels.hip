@@ -24,6 +24,7 @@
 
 #include "rxg_common.h"
 #include "rxg_kernels.h"
+#include "rxg_mirror.h"
 
 namespace rxg {
 
@@ -1267,7 +1268,6 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     const uint32_t nslices = (L.n + 63u) / 64u;
     uint32_t blocks = (nslices + 3u) / 4u;
     if (blocks > L.max_blocks) blocks = L.max_blocks;
-    // L.variant: experiment builds only (a class subset; frames of other classes are skipped)
     // production kernels use non-temporal loads for the >256 B classes (measured +5 %
     // at 1500 B, -4 % at 64 B: classes 0-2 always use plain loads)
     if (L.sel) {  // re-classification of selected frames (rxg_rx_replay), records of 16 B
@@ -1275,7 +1275,9 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         return hipGetLastError();
     }
     if (L.mode == 16) {
-        // experiment variants (RXG_VARIANT, scripts/kbench.py); 0 = production.  1-3: class
+#ifdef RXG_EXPERIMENTS
+        // experiment variants (RXG_VARIANT, scripts/kbench.py; experiment library only: a
+        // class subset skips the frames of other classes); 0 = production.  1-3: class
         // subsets / plain loads; 8-10: C3 ablations (STRIP 2 no TCB probe, 4 no record
         // store, 8 no phase B)
         switch (L.variant) {
@@ -1287,11 +1289,39 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 10: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 8>), dim3(blocks), dim3(256), 0, st, a); break;
         default: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
+#else
+        hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
+#endif
     } else if (L.mode == 48) {
         hipLaunchKernelGGL((rx_kernel<48, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     } else {
         hipLaunchKernelGGL((rx_kernel<0, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     }
+    return hipGetLastError();
+}
+
+// The device words a batch of TCB / ARP mirror writes changed (rxg_mirror.h), one thread per
+// patch; the host deduplicated them, so no two threads write the same word.  The patch list
+// is read straight from pinned host memory (a few hundred bytes per burst).
+__global__ __launch_bounds__(256) void mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets,
+                                                    int32_t *listen, uint2 *arp)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const MirrorPatch q = p[i];
+    if (q.target == kPatchBucket)
+        buckets[q.index] = make_uint4(q.v[0], q.v[1], q.v[2], q.v[3]);
+    else if (q.target == kPatchListen)
+        listen[q.index] = (int32_t)q.v[0];
+    else
+        arp[q.index] = make_uint2(q.v[0], q.v[1]);
+}
+
+hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets, int32_t *listen, uint2 *arp,
+                               hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(mirror_patch, dim3((n + 255u) / 256u), dim3(256), 0, st, p, n, buckets, listen, arp);
     return hipGetLastError();
 }
 

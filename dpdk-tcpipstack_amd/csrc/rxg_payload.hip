@@ -594,12 +594,18 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     *launched = 0;
     hipError_t e = hipMemsetAsync(P.used, 0, sizeof(unsigned long long), st);
     if (e != hipSuccess || P.n == 0) return e;
-    const int fpt = (P.variant == 6 || P.variant == 7) ? 4 : 1;
+#ifdef RXG_EXPERIMENTS
+    const int variant = P.variant;
+#else
+    const int variant = 0;
+#endif
+    const int fpt = (variant == 6 || variant == 7) ? 4 : 1;
     // workgroup size of the kernel the switch below launches
-    const int tpb = (P.variant >= 1 && P.variant <= 10) ? kPgThreads : P.variant == 12 ? 512 : kPgThreadsProd;
+    const int tpb = (variant >= 1 && variant <= 10) ? kPgThreads : variant == 12 ? 512 : kPgThreadsProd;
     a.nblocks = (P.n + tpb * fpt - 1) / (tpb * fpt);
     const dim3 g(a.nblocks), b(tpb);
-    switch (P.variant) {  // experiment variants (RXG_PG_VARIANT); 0 = production
+#ifdef RXG_EXPERIMENTS
+    switch (variant) {  // experiment variants (RXG_PG_VARIANT, experiment library only)
     case 1: hipLaunchKernelGGL((pg_gather<4, false, 1, true>), g, b, 0, st, a); break;
     case 5: hipLaunchKernelGGL((pg_gather<4, true, 1, false>), g, b, 0, st, a); break;
     case 6: hipLaunchKernelGGL((pg_gather<4, true, 4, true>), g, b, 0, st, a); break;
@@ -611,7 +617,10 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     case 12: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 512>), g, b, 0, st, a); break;
     default: hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
     }
-    *launched = (a.ticket && (P.variant != 5 && P.variant != 7)) ? a.nblocks : 0u;
+#else
+    hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
+#endif
+    *launched = (a.ticket && (variant != 5 && variant != 7)) ? a.nblocks : 0u;
     return hipGetLastError();
 }
 

@@ -5,11 +5,13 @@
  * (tcp_listen allocates a child TCB from a SYN, tcp_syn_rcv establishes it, a FIN closes a
  * flow, tcp_closed removes it), each mirroring its tcbs[] write with rxg_tcb_*.
  *
- *   rx_loop IN OUT BURST
+ *   rx_loop IN OUT BURST [verify]
  *   IN : u32 nrows; nrows x {i32 dport, i32 sport, u32 ipv4_dst (raw), u32 ipv4_src (host),
  *        u8 state, u8 live, u16 pad}; u32 nframes; nframes x {u16 len, len bytes}
  *   OUT: nframes x {u8 kind (0 none, 1 freed, 2 reset, 3 tcpswitch), u8 state, u16 pad,
- *        i32 tcb_idx}; then u32 ntcb and the final table in IN's row format.
+ *        i32 tcb_idx}; then u32 ntcb and the final table in IN's row format; then the
+ *        reference's rx counters i32 tcpnopcb, i32 tcpchecksumerror (tcp_in.c:18-19).
+ *   verify: tcp_in.c:37-41 compiled in (RXG_OPS_VERIFY_TCP_CKSUM).
  * Exit status: 0 ok, 2 usage/input error, 3 rxg error (message on stderr; 3 without a GPU).
  */
 #include <stdint.h>
@@ -35,6 +37,8 @@ struct out_rec {
 };
 
 static struct row *tcbs;  /* tcbs[] and Ntcb of tcp_tcb.c:21-22 */
+int tcpchecksumerror;     /* tcp_in.c:18, extern in tcp_in.h:7 */
+int tcpnopcb;             /* tcp_in.c:19, extern in tcp_in.h:11 */
 static int32_t ntcb, cap;
 static rxg_ctx *g_rxg;
 static struct out_rec *g_out;
@@ -108,8 +112,8 @@ static int ops_switch(void *u, int32_t idx, uint8_t st, void *tcp, void *ip, voi
 
 int main(int argc, char **argv)
 {
-    if (argc != 4) {
-        fprintf(stderr, "usage: rx_loop IN OUT BURST\n");
+    if (argc != 4 && !(argc == 5 && strcmp(argv[4], "verify") == 0)) {
+        fprintf(stderr, "usage: rx_loop IN OUT BURST [verify]\n");
         return 2;
     }
     const uint32_t burst = (uint32_t)atoi(argv[3]);
@@ -132,7 +136,7 @@ int main(int argc, char **argv)
     }
     fclose(in);
 
-    rxg_config cfg = {0, burst, 0, 0};
+    rxg_config cfg = {.device = 0, .max_batch = burst};
     if (rxg_init(&cfg, &g_rxg) != 0) {
         fprintf(stderr, "rxg_init: %s\n", rxg_last_error());
         return 3;
@@ -158,7 +162,12 @@ int main(int argc, char **argv)
     rxg_pkt_view *views = calloc(burst, sizeof *views);
     rxg_rec16 *recs = calloc(burst, sizeof *recs);
     void **mbufs = calloc(burst, sizeof *mbufs), **frames = calloc(burst, sizeof *frames);
-    rxg_handoff_ops ops = {NULL, ops_free, NULL, NULL, NULL, ops_rst, NULL, ops_switch};
+    rxg_handoff_ops ops = {.free_mbuf = ops_free,
+                           .send_reset = ops_rst,
+                           .tcpswitch = ops_switch,
+                           .tcpnopcb = &tcpnopcb,
+                           .tcpchecksumerror = &tcpchecksumerror,
+                           .flags = argc == 5 ? RXG_OPS_VERIFY_TCP_CKSUM : 0u};
     for (uint32_t b0 = 0; b0 < n; b0 += burst) { /* l2fwd_main_loop, main.c:391-399 */
         const uint32_t nb = n - b0 < burst ? n - b0 : burst;
         g_base = b0;
@@ -181,6 +190,8 @@ int main(int argc, char **argv)
     fwrite(g_out, sizeof *g_out, n, out);
     fwrite(&ntcb, 4, 1, out);
     fwrite(tcbs, sizeof *tcbs, (size_t)ntcb, out);
+    fwrite(&tcpnopcb, 4, 1, out);
+    fwrite(&tcpchecksumerror, 4, 1, out);
     fclose(out);
     rxg_fini(g_rxg);
     return 0;

@@ -60,9 +60,12 @@ class RxgError(RuntimeError):
 
 
 # ------------------------------------------------------------------- ctypes structs ---
+ABI_VERSION = 2
+
+
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("max_batch", C.c_uint32), ("max_bytes", C.c_uint32),
-                ("flags", C.c_uint32)]
+                ("flags", C.c_uint32), ("max_blocks", C.c_uint32), ("zc_bytes", C.c_uint32)]
 
 
 class TcbTuple(C.Structure):
@@ -125,7 +128,13 @@ class HandoffOps(C.Structure):
     _fields_ = [("user", C.c_void_p), ("free_mbuf", HANDOFF_FREE), ("arp_in", HANDOFF_ARP_IN),
                 ("get_mac", HANDOFF_GET_MAC), ("add_mac", HANDOFF_ADD_MAC),
                 ("send_reset", HANDOFF_SEND_RESET), ("on_segment", HANDOFF_ON_SEGMENT),
-                ("tcpswitch", HANDOFF_TCPSWITCH)]
+                ("tcpswitch", HANDOFF_TCPSWITCH),
+                # tcp_in.c:18-19 globals (int*), bumped by the replay; NULL = not kept
+                ("tcpnopcb", C.POINTER(C.c_int)), ("tcpchecksumerror", C.POINTER(C.c_int)),
+                ("flags", C.c_uint32)]
+
+
+OPS_VERIFY_TCP_CKSUM = 0x1  # rxg_handoff_ops.flags: tcp_in.c:37-41 compiled in
 
 
 # ------------------------------------------------------------------------- loading ---
@@ -221,8 +230,8 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rxg_abi_version() != 1:
-        raise RxgError("librxg ABI version mismatch")
+    if lib.rxg_abi_version() != ABI_VERSION:
+        raise RxgError(f"librxg ABI version {lib.rxg_abi_version()}, binding expects {ABI_VERSION}")
     _lib = lib
     return lib
 
@@ -338,9 +347,10 @@ class PinnedArray:
 class Engine:
     """One rxg context on one GPU (include/rxg.h: rxg_init .. rxg_fini)."""
 
-    def __init__(self, device: int = 0, max_batch: int = 0, max_bytes: int = 0):
+    def __init__(self, device: int = 0, max_batch: int = 0, max_bytes: int = 0,
+                 max_blocks: int = 0, zc_bytes: int = 0):
         load_library()
-        cfg = Config(device, max_batch, max_bytes, 0)
+        cfg = Config(device, max_batch, max_bytes, 0, max_blocks, zc_bytes)
         ctx = C.c_void_p()
         _check(_lib.rxg_init(C.byref(cfg), C.byref(ctx)), "rxg_init")
         self.ctx = ctx.value
@@ -597,7 +607,7 @@ class Group:
     def __init__(self, devices, max_batch: int = 0, max_bytes: int = 0):
         load_library()
         devs = (C.c_int32 * len(devices))(*devices)
-        cfg = Config(0, max_batch, max_bytes, 0)
+        cfg = Config(0, max_batch, max_bytes, 0, 0, 0)
         g = C.c_void_p()
         _gcheck(_lib.rxg_group_init(devs, len(devices), C.byref(cfg), C.byref(g)), "rxg_group_init")
         self.g = g.value

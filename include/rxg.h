@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RXG_ABI_VERSION 1
+#define RXG_ABI_VERSION 2
 
 /* ------------------------------------------------------------------------- */
 /* Protocol constants (wire formats; reference names in comments).            */
@@ -171,6 +171,10 @@ typedef struct rxg_config {
     uint32_t max_batch;    /* largest n passed to the host-buffer entry points (staging)   */
     uint32_t max_bytes;    /* staging arena bytes for host-buffer entry points            */
     uint32_t flags;        /* reserved, 0                                                  */
+    uint32_t max_blocks;   /* rx grid cap in workgroups; 0 = one generation of resident
+                              workgroups (occupancy).  Any value gives the same records.   */
+    uint32_t zc_bytes;     /* rxg_rx_burst: bursts of up to this many staged bytes run
+                              zero-copy (kernel reads pinned staging over PCIe); 0 = 64 MiB */
 } rxg_config;
 
 int rxg_abi_version(void);
@@ -208,7 +212,11 @@ int rxg_tcb_remove(rxg_ctx *ctx, int32_t idx);
 int rxg_tcb_set_state(rxg_ctx *ctx, int32_t idx, uint8_t state);
 /* Replace the whole table: tcbs[0..ntcb), live[i]==0 marks a NULL slot. */
 int rxg_tcb_load(rxg_ctx *ctx, const rxg_tcb_tuple *tcbs, const uint8_t *live, int32_t ntcb);
-/* Push pending mirror changes to the device (done implicitly by every burst). */
+/* Push pending mirror changes to the device (done implicitly by every burst).  Each write
+   changes O(1) device words (a bucket slot, a listener entry), applied by one small kernel
+   on the context's stream after every launch that still reads the old table, whatever its
+   stream; a burst on another stream waits for them on the device, not on the host.  Only
+   rxg_tcb_load and growth past load 1/2 rebuild (and upload) the whole table. */
 int rxg_tcb_sync(rxg_ctx *ctx);
 /* Current Ntcb of the mirror. */
 int32_t rxg_tcb_count(rxg_ctx *ctx);
@@ -331,7 +339,20 @@ typedef struct rxg_handoff_ops {
     /* tcpswitch[state](tcb, tcp_hdr, ip_hdr, mbuf)             tcp_states.c:257-265 */
     int (*tcpswitch)(void *user, int32_t tcb_idx, uint8_t state, void *tcp_hdr, void *ip_hdr,
                      void *mbuf);
+    /* The reference's rx counters, globals of tcp_in.c:18-19 exported at tcp_in.h:7,11.  The
+       replay increments them where tcp_in does, in packet order: *tcpnopcb at every findtcb
+       miss (tcp_in.c:47-48); *tcpchecksumerror only with RXG_OPS_VERIFY_TCP_CKSUM, at every
+       TCP segment whose checksum fails (tcp_in.c:37-40).  NULL: not kept. */
+    int *tcpnopcb;
+    int *tcpchecksumerror;
+    uint32_t flags;      /* RXG_OPS_* */
 } rxg_handoff_ops;
+
+/* rxg_handoff_ops.flags.  RXG_OPS_VERIFY_TCP_CKSUM turns on the block tcp_in.c:37-41 compiles
+   out (`if(0)`): a TCP segment whose pseudo || segment checksum is not 0x0000 (record flag
+   RXG_F_TCP_OK clear) is freed and counted in *tcpchecksumerror after ip_in's ARP learn,
+   before findtcb -- no reset, no hand-off.  Off (0) is the reference as shipped. */
+#define RXG_OPS_VERIFY_TCP_CKSUM 0x1u
 
 /* Performs, in packet order, the side effects ether_in() would have performed for
    pkts[0..n) given their records.  frames[i] = the frame bytes of mbufs[i].  It must
@@ -386,15 +407,20 @@ typedef struct rxg_payload_out {
     uint64_t arena_cap;      /* bytes                                                       */
     rxg_payload_msg *msgs;   /* dev, one per frame of the burst (flags 0: not gathered)      */
     uint64_t *arena_used;    /* dev, 1 entry: bytes the burst's candidates need; frames past
-                                arena_cap are not gathered                                  */
+                                arena_cap are not gathered.  UINT64_MAX (~0): the gather's
+                                offset look-back timed out (a workgroup never published), so
+                                arena offsets are unreliable; rxg_payload_take then refuses
+                                every payload of the burst (the stack's own PushData runs)   */
 } rxg_payload_out;
 
 /* Gathers, for the LAST burst on this context (rxg_rx_burst or rxg_rx_burst_dev; its
    device batch and records must still be valid), the payload of every TCP segment
    (verdict DISPATCH, RST_NOPCB or RST_LISTEN_NONSYN -- the replay may turn the latter into
    a DISPATCH) with datalen > 0 and the payload inside the frame.  Packet order;
-   asynchronous on `stream`.  o->msgs must stay valid until the burst's replay is done:
-   the first rxg_payload_take after the gather copies the descriptors to the host. */
+   asynchronous on `stream`.  o->msgs and o->arena_used must stay valid until the burst's
+   replay is done: the first rxg_payload_take after the gather copies them to the host.
+   One gather is in flight per context: a gather waits (on the device) for the previous
+   one, whatever streams they were issued on. */
 int rxg_payload_gather_dev(rxg_ctx *ctx, const rxg_payload_out *o, void *stream);
 
 /* Receive-window mirror: ReceiveWindow.CurrentSequenceNumber of tcbs[idx] and whether its

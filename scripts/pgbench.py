@@ -11,6 +11,8 @@ import torch  # noqa: F401  (one HIP runtime per process)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")]
+# the experiment library (make -C dpdk-tcpipstack_amd experiments): the variant switches
+os.environ.setdefault("RXG_LIB", os.path.join(ROOT, "dpdk-tcpipstack_amd", "rxg", "librxg_exp.so"))
 import rxg  # noqa: E402
 
 WL = {"c3": (1500, 1000, 0), "c2": (64, 1, 0), "c4": (0, 65536, 1)}

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Tx checksum-generate micro-benchmark: rxg_tx_cksum_dev over the C3 / C4 batch, one rxg
-context per RXG_MAX_BLOCKS value (0 = occupancy grid), interleaved rounds.
+context per grid cap (rxg_config.max_blocks) (0 = occupancy grid), interleaved rounds.
   python scripts/txbench.py --grids 0,768 --workloads c3,c4
 A grid may name another librxg build as GRID:PATH (A/B of two builds in one process)."""
 import argparse
@@ -29,14 +29,13 @@ def main():
     main_lib = rxg.load_library()
     for g in args.grids.split(","):
         grid, _, path = g.partition(":")
-        os.environ["RXG_MAX_BLOCKS"] = grid
         lib = main_lib
         if path:
             rxg._lib = None
             lib = rxg.load_library(path)
         rxg._lib = lib
         libs[g] = lib
-        engs[g] = rxg.Engine(0)
+        engs[g] = rxg.Engine(0, max_blocks=int(grid or 0))
         rxg._lib = main_lib
     base = engs[args.grids.split(",")[0]]
     rxg._lib = libs[args.grids.split(",")[0]]

@@ -45,7 +45,7 @@ def test_library_has_gfx950_code_object():
 
 def test_abi_version_and_build_info():
     lib = rxg.load_library()
-    assert lib.rxg_abi_version() == 1
+    assert lib.rxg_abi_version() == rxg.ABI_VERSION == 2
     assert b"gfx950" in lib.rxg_build_info()
 
 
@@ -129,3 +129,59 @@ def test_pack_arena_layout():
     arena, off, lens = rxg.pack_arena(frames)
     assert off.tolist() == [0, 1, 2, 4] and lens.tolist() == [10, 64, 65, 0]
     assert arena.size == 4 * 64 and bytes(arena[128:193]) == b"c" * 65
+
+
+EXPERIMENT_SWITCHES = [b"RXG_VARIANT", b"RXG_NOCOUNT", b"RXG_PG_VARIANT", b"RXG_MAX_BLOCKS", b"RXG_ZC_BYTES"]
+
+
+def _kernel_instantiations(path):
+    """(MODE, CMASK, NT, STRIP) of every rx_kernel in the library's gfx950 code object."""
+    data = open(path, "rb").read()
+    return set(re.findall(rb"rx_kernelILi(\d+)ELi(\d+)ELb(\d)ELi(\d+)E", data))
+
+
+def test_product_library_has_no_experiment_switches():
+    """librxg.so reads no environment variable that changes what a burst computes and holds
+    only the production kernels: every rx_kernel handles every size class (CMASK 255) and
+    strips nothing (STRIP 0).  The variants live in the experiment build (librxg_exp.so,
+    make experiments) that scripts/kbench.py and pgbench.py load."""
+    data = open(rxg.LIB_PATH, "rb").read()
+    for sw in EXPERIMENT_SWITCHES:
+        assert sw not in data, sw
+    inst = _kernel_instantiations(rxg.LIB_PATH)
+    assert inst, "no rx_kernel found in the code object"
+    assert all(cmask == b"255" and strip == b"0" for _, cmask, _, strip in inst), inst
+    assert re.findall(rb"pg_gather", data)
+
+
+def test_experiment_library_is_separate():
+    exp = os.path.join(os.path.dirname(rxg.LIB_PATH), "librxg_exp.so")
+    if not os.path.exists(exp):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "dpdk-tcpipstack_amd"), "experiments"], check=True)
+    data = open(exp, "rb").read()
+    assert all(sw in data for sw in EXPERIMENT_SWITCHES)
+    assert any(strip != b"0" for _, _, _, strip in _kernel_instantiations(exp))
+
+
+def test_handoff_ops_layout_matches_header():
+    """rxg_handoff_ops grew the reference's rx counters (tcp_in.c:18-19) and a flags word."""
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "rxg.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(rxg_handoff_ops), offsetof(rxg_handoff_ops, tcpnopcb),
+         offsetof(rxg_handoff_ops, tcpchecksumerror), offsetof(rxg_handoff_ops, flags),
+         sizeof(rxg_config), offsetof(rxg_config, zc_bytes));
+  return 0;
+}'''
+    tmp = os.path.join(ROOT, "build_abi_probe")
+    os.makedirs(tmp, exist_ok=True)
+    with open(os.path.join(tmp, "h.c"), "w") as fh:
+        fh.write(src)
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), os.path.join(tmp, "h.c"), "-o",
+                    os.path.join(tmp, "h")], check=True)
+    got = [int(x) for x in subprocess.run([os.path.join(tmp, "h")], capture_output=True, text=True).stdout.split()]
+    H = rxg.HandoffOps
+    assert got == [C.sizeof(H), H.tcpnopcb.offset, H.tcpchecksumerror.offset, H.flags.offset,
+                   C.sizeof(rxg.Config), rxg.Config.zc_bytes.offset]

@@ -35,7 +35,7 @@ def _write_input(path, rows, frames):
             fh.write(struct.pack("<H", len(f)) + f)
 
 
-def _read_output(path, n):
+def _read_output(path, n, with_globals=False):
     data = open(path, "rb").read()
     out = np.frombuffer(data[: n * OUT.itemsize], dtype=OUT)
     (ntcb,) = struct.unpack_from("<I", data, n * OUT.itemsize)
@@ -43,6 +43,9 @@ def _read_output(path, n):
     for i in range(ntcb):
         d, s, dst, src, st, live, _ = ROW.unpack_from(data, n * OUT.itemsize + 4 + i * ROW.size)
         rows.append((d, s, dst, src, st) if live else None)
+    if with_globals:  # the reference's rx globals tcpnopcb, tcpchecksumerror (tcp_in.c:18-19)
+        g = struct.unpack_from("<ii", data, n * OUT.itemsize + 4 + ntcb * ROW.size)
+        return out, rows, {"tcpnopcb": g[0], "tcpchecksumerror": g[1]}
     return out, rows
 
 
@@ -68,6 +71,38 @@ def test_c_loop_equals_sequential_reference(tmp_path, burst):
     r = subprocess.run([_exe(), str(inp), str(outp), str(burst)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     out, got_rows = _read_output(outp, len(frames))
+    for i, (v, idx, st) in enumerate(exp):
+        if v == rxg.V_DISPATCH:
+            assert (out["kind"][i], out["tcb_idx"][i], out["state"][i]) == (3, idx, st), (i, out[i], exp[i])
+        elif v in (rxg.V_RST_NOPCB, rxg.V_RST_LISTEN_NONSYN):
+            assert out["kind"][i] == 2, (i, out[i], exp[i])
+        else:
+            assert out["kind"][i] == 1, (i, out[i], exp[i])
+    assert [None if x is None else (x[0], x[1], x[2] & 0xFFFFFFFF, x[3] & 0xFFFFFFFF, x[4]) for x in erows] == \
+        [None if x is None else tuple(x) for x in got_rows]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("verify", [False, True])
+def test_c_loop_reference_rx_counters(tmp_path, verify):
+    """tcpnopcb / tcpchecksumerror (tcp_in.c:18-19, extern in tcp_in.h:7,11) stay linkable
+    and correct behind the replaced loop: the C program hands their addresses to the replay
+    (rxg_handoff_ops), which bumps them in packet order exactly where tcp_in does -- with
+    the reference's `if(0)` (verify off) and with the check compiled in (verify on: bad
+    TCP checksums freed before findtcb, no reset, no hand-off)."""
+    from test_gpu_replay import scenario, sequential_reference
+    import rxg
+    rows, frames = scenario(11, n=1500, corrupt=0.08, closed=0.1)
+    g_exp = {}
+    exp, _, erows = sequential_reference(rows, frames, verify=verify, globals_out=g_exp)
+    assert g_exp["tcpnopcb"] > 0 and (g_exp["tcpchecksumerror"] > 0) == verify
+    inp, outp = tmp_path / "in.bin", tmp_path / "out.bin"
+    _write_input(inp, rows, frames)
+    args = [_exe(), str(inp), str(outp), "32"] + (["verify"] if verify else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out, got_rows, g_got = _read_output(outp, len(frames), with_globals=True)
+    assert g_got == g_exp
     for i, (v, idx, st) in enumerate(exp):
         if v == rxg.V_DISPATCH:
             assert (out["kind"][i], out["tcb_idx"][i], out["state"][i]) == (3, idx, st), (i, out[i], exp[i])

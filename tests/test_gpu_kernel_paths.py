@@ -10,7 +10,6 @@ reach:
 
 Everything is compared bit-exact, records and counters, with the oracle.
 """
-import os
 import random
 
 import numpy as np
@@ -25,17 +24,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module", params=[1, 3])
 def small_grid_engine(request):
-    """A context whose rx grid is `param` workgroups (RXG_MAX_BLOCKS is read when the
-    context is created): 4 or 12 waves, so each wave walks many slices."""
-    old = os.environ.get("RXG_MAX_BLOCKS")
-    os.environ["RXG_MAX_BLOCKS"] = str(request.param)
-    try:
-        eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20)
-    finally:
-        if old is None:
-            del os.environ["RXG_MAX_BLOCKS"]
-        else:
-            os.environ["RXG_MAX_BLOCKS"] = old
+    """A context whose rx grid is `param` workgroups (rxg_config.max_blocks): 4 or 12 waves,
+    so each wave walks many slices."""
+    eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20, max_blocks=request.param)
     yield eng
     eng.close()
 

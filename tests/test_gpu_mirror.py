@@ -1,0 +1,154 @@
+"""GPU: the incremental device TCB mirror (csrc/rxg_mirror.h) under live churn, and the
+ordering of mirror writes against bursts on other streams.
+
+* Churn: a 65 537-TCB table (the C4 flow count) takes rounds of the writes the reference
+  makes -- tcp_listen appending children (tcp_states.c:150-207), remove_tcb NULLing slots
+  (tcp_tcb.c:175-186), tuple rewrites (tcp_states.c:25-27), state changes, listeners coming
+  and going -- each applied as O(1) device patches, never a reload.  After every round a
+  burst is compared bit-exact (REC48 + counters) with the oracle's findtcb over the table as
+  it stands.
+* Ordering: a long burst on a caller stream is still running when the table changes; it must
+  classify against the old table, and the next burst (same stream, another stream, or the
+  context's) against the new one, with no host synchronisation in between.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import pktgen
+import rxg
+
+pytestmark = pytest.mark.gpu
+DST = pktgen.ip4(192, 168, 78, 2)
+DST_RAW = pktgen.raw_of_host(DST)
+
+
+def _frames(rng, rows, n):
+    """Frames aimed at live flows, dead flows, never-seen flows and listeners."""
+    out = []
+    for _ in range(n):
+        k = rng.random()
+        if k < 0.6:
+            r = rows[rng.randrange(len(rows))]
+            if r is None or r[1] < 0 or r[1] > 65535 or r[0] < 0 or r[0] > 65535:
+                r = (80, 1024, DST_RAW, pktgen.ip4(10, 0, 0, 1), 4)
+            out.append(pktgen.frame(src_ip=r[3], dst_ip=DST, sport=r[1], dport=r[0],
+                                    flags=rng.choice([0x10, 0x18, 0x02, 0x11])))
+        elif k < 0.85:
+            out.append(pktgen.frame(src_ip=pktgen.ip4(172, 16, rng.randrange(256), rng.randrange(256)),
+                                    dst_ip=DST, sport=rng.randrange(1024, 65536),
+                                    dport=rng.choice([80, 80, 8080, 9000]), flags=rng.choice([0x02, 0x10])))
+        else:
+            out.append(pktgen.frame(src_ip=pktgen.ip4(10, 0, rng.randrange(256), rng.randrange(256)),
+                                    dst_ip=DST, sport=1024 + rng.randrange(64511), dport=80, flags=0x10))
+    return out
+
+
+def _check_burst(eng, rows, frames):
+    tcb, live = pktgen.table_arrays(rows)
+    arena, off, lens = pktgen.pack_arena(frames)
+    eng.counters_reset()
+    got = eng.rx_arena(arena, off, lens, rxg.REC48)
+    cnt = eng.counters()
+    exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+    if got.tobytes() != exp.tobytes():
+        bad = np.nonzero(got.view(np.uint8).reshape(len(frames), 48) != exp.view(np.uint8).reshape(len(frames), 48))[0]
+        i = int(bad[0])
+        raise AssertionError(f"{len(set(bad.tolist()))} records differ; first {i}: {got[i]} vs {exp[i]}")
+    assert cnt.tolist() == ecnt.tolist()
+
+
+def test_churn_incremental_mirror_equals_oracle(engine):
+    rng = random.Random(2024)
+    nflows = 65536
+    t0, l0 = rxg.synthetic_tcb_table(nflows)
+    rows = [(int(t["dport"]), int(t["sport"]), int(t["ipv4_dst"]), int(t["ipv4_src"]), int(t["state"]))
+            for t in t0]
+    engine.tcb_load(t0, l0)
+    engine.tcb_sync()
+    for rnd in range(12):
+        for _ in range(rng.choice([1, 8, 64, 300])):
+            k = rng.random()
+            n = len(rows)
+            if k < 0.35:    # tcp_listen: a child at Ntcb (sometimes a duplicate tuple: SYN resent)
+                src = pktgen.ip4(172, 16, rng.randrange(256), rng.randrange(256))
+                r = (80, rng.randrange(1024, 65536), DST_RAW, src, rng.choice([3, 4]))
+                if rng.random() < 0.1:
+                    live_rows = [x for x in rows[1:200] if x is not None]
+                    r = live_rows[rng.randrange(len(live_rows))][:4] + (3,)
+                rows.append(r)
+                engine.tcb_upsert(n, *r)
+            elif k < 0.6:   # remove_tcb
+                i = rng.randrange(n)
+                if rows[i] is not None:
+                    rows[i] = None
+                    engine.tcb_remove(i)
+            elif k < 0.75:  # tuple rewrite of a live slot (tcp_syn_sent) or reuse of a NULL slot
+                i = rng.randrange(1, n)
+                r = (rng.choice([80, 8080, 9000]), rng.randrange(1024, 65536), DST_RAW,
+                     pktgen.ip4(10, 9, rng.randrange(256), rng.randrange(256)), rng.randrange(7))
+                rows[i] = r
+                engine.tcb_upsert(i, *r)
+            else:           # state change, listeners included
+                i = rng.randrange(n)
+                if rows[i] is not None:
+                    st = rng.choice([0, 1, 3, 4, 5, 6])
+                    rows[i] = rows[i][:4] + (st,)
+                    engine.tcb_set_state(i, st)
+        _check_burst(engine, rows, _frames(rng, rows, 3000))
+    # the patched table equals a fresh full build of the same rows
+    tcb, live = pktgen.table_arrays(rows)
+    frames = _frames(rng, rows, 3000)
+    arena, off, lens = pktgen.pack_arena(frames)
+    a = engine.rx_arena(arena, off, lens, rxg.REC48)
+    engine.tcb_load(tcb, live)
+    b = engine.rx_arena(arena, off, lens, rxg.REC48)
+    assert a.tobytes() == b.tobytes()
+
+
+@pytest.mark.parametrize("second", ["same", "other", "ctx"])
+def test_mirror_write_between_bursts_on_caller_streams(engine, second):
+    """a mirror write must neither reach a burst still running on a caller stream
+    nor be missed by the next burst, without the caller synchronising."""
+    n, nflows = 1 << 20, 1000
+    dev = engine.synth(n=n, nflows=nflows, len_a=1500, seed=77, with_flows=True)
+    t0, l0 = rxg.synthetic_tcb_table(nflows)
+    engine.tcb_load(t0, l0)
+    engine.tcb_sync()
+    engine.sync()
+    flows = dev["flow"].download(np.uint32, n)
+    out_a, out_b = engine.alloc(n * 16), engine.alloc(n * 16)
+    s1 = torch.cuda.Stream()
+    s2 = torch.cuda.Stream()
+    try:
+        for _ in range(3):  # a few rounds: the first burst is long (≈250 us), the writes are µs
+            engine.tcb_load(t0, l0)
+            engine.tcb_sync()
+            engine.sync()
+            torch.cuda.synchronize()
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out_a.ptr, 16,
+                                s1.cuda_stream)
+            removed = list(range(1, nflows + 1, 3))
+            for i in removed:       # flows 0, 3, 6, ... lose their TCB
+                engine.tcb_remove(i)
+            stream_b = {"same": s1.cuda_stream, "other": s2.cuda_stream, "ctx": None}[second]
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out_b.ptr, 16, stream_b)
+            torch.cuda.synchronize()
+            engine.sync()
+            a = out_a.download(rxg.REC16_DTYPE, n)
+            b = out_b.download(rxg.REC16_DTYPE, n)
+            assert (a["tcb_idx"] == flows.astype(np.int32) + 1).all()
+            assert (a["verdict"] == rxg.V_DISPATCH).all()
+            gone = (flows % 3) == 0
+            assert (b["tcb_idx"][~gone] == flows[~gone].astype(np.int32) + 1).all()
+            # a removed flow falls to the listener (slot 0) as a non-SYN: reset (tcp_in.c:54-59)
+            assert (b["tcb_idx"][gone] == 0).all() and (b["verdict"][gone] == rxg.V_RST_LISTEN_NONSYN).all()
+    finally:
+        for d in (out_a, out_b):
+            d.free()
+        for v in dev.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()

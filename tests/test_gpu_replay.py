@@ -57,7 +57,10 @@ class Model:
                 self.eng.tcb_remove(idx)
 
 
-def scenario(seed, nflows=40, n=1500):
+def scenario(seed, nflows=40, n=1500, corrupt=0.0, closed=0.0):
+    """Flows, listeners, unknown clients; `corrupt`: share of frames with one payload or
+    header byte flipped after the checksums were filled (a bad TCP checksum); `closed`:
+    share of client frames sent to a port nobody listens on (findtcb NULL, tcp_in.c:47)."""
     rng = random.Random(seed)
     dst = pktgen.ip4(192, 168, 78, 2)
     rows = [(80, 0, pktgen.raw_of_host(dst), 0, LISTENING)]
@@ -78,26 +81,46 @@ def scenario(seed, nflows=40, n=1500):
             src, sport = rng.choice(clients)
             fl = rng.choice([0x02, 0x10, 0x10, 0x18, 0x11])
         dport = 8080 if rng.random() < 0.1 else 80
-        frames.append(pktgen.frame(src_ip=src, dst_ip=dst, sport=sport, dport=dport, flags=fl,
-                                   seq=rng.getrandbits(32), ack=rng.getrandbits(32),
-                                   payload=rng.randbytes(rng.randrange(0, 200))))
+        if closed and k >= 0.35 and rng.random() < closed:
+            dport = 9999
+        f = pktgen.frame(src_ip=src, dst_ip=dst, sport=sport, dport=dport, flags=fl,
+                         seq=rng.getrandbits(32), ack=rng.getrandbits(32),
+                         payload=rng.randbytes(rng.randrange(0, 200)))
+        if corrupt and rng.random() < corrupt:
+            b = bytearray(f)
+            b[rng.randrange(38, len(b))] ^= 0x5A   # seq/ack/flags/payload: TCP checksum only
+            f = bytes(b)
+        frames.append(f)
     return rows, frames
 
 
-def sequential_reference(rows, frames):
+def sequential_reference(rows, frames, verify=False, globals_out=None):
     """The reference loop: classify packet i against the table as it is NOW, then run its
-    handler.  Returns per-packet (verdict, tcb_idx, state) and the summed counters."""
+    handler.  Returns per-packet (verdict, tcb_idx, state) and the summed counters.
+    verify: tcp_in.c:37-40 compiled in -- a TCP segment with a bad checksum is freed before
+    findtcb (verdict reported as V_DROP_NONTCP, "freed").  globals_out (dict) receives the
+    reference's rx globals tcpnopcb (tcp_in.c:48) and tcpchecksumerror (:39)."""
     m = Model(rows)
     out, cnt = [], np.zeros(16, dtype=np.uint64)
+    nopcb = cksumerr = 0
     for f in frames:
         arena, off, lens = pktgen.pack_arena([f])
         tcb, live = pktgen.table_arrays(m.rows)
         rec, c = oracle.rx_batch(arena, off, lens, tcb, live)
         cnt += c
         r = rec[0]["c"]
-        out.append((int(r["verdict"]), int(r["tcb_idx"]), int(r["state"])))
+        v = int(r["verdict"])
+        if verify and v in (rxg.V_DISPATCH, rxg.V_RST_NOPCB, rxg.V_RST_LISTEN_NONSYN) \
+                and not (r["flags"] & rxg.F_TCP_OK):
+            cksumerr += 1
+            out.append((rxg.V_DROP_NONTCP, -1, rxg.STATE_NONE))
+            continue
+        nopcb += v == rxg.V_RST_NOPCB
+        out.append((v, int(r["tcb_idx"]), int(r["state"])))
         if r["verdict"] == rxg.V_DISPATCH:
             m.handle(int(r["tcb_idx"]), int(r["state"]), f)
+    if globals_out is not None:
+        globals_out.update(tcpnopcb=nopcb, tcpchecksumerror=cksumerr)
     return out, cnt, m.rows
 
 
