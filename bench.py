@@ -71,6 +71,14 @@ def max_over_ranks(x: float, device) -> float:
     return float(t.item())
 
 
+def min_over_ranks(x: float, device) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def sum_over_ranks(x: float, device) -> float:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return x
@@ -307,6 +315,31 @@ def tx_leg(eng, wl, steps, warmup):
             "roofline_frac": round(wl.bytes_per_batch / k / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def replay_churn_leg():
+    """SURVEY.md 8(f) row 2 under load: burst + in-order replay (rxg_rx_replay) with C
+    handlers shaped like tcp_states.c's, 1 % of the frames starting a connection event (a new
+    client's SYN + ACK: tcp_listen appends a child, tcp_syn_rcv establishes it; or an
+    established flow's FIN + next segment: CLOSED, then remove_tcb), at the C4 and C5 table
+    sizes, 4 096-frame bursts of 64 B frames, beside the same run without churn.  Runs
+    dpdk-tcpipstack_amd/build/churn_bench (a child process on the same GPU)."""
+    import subprocess
+    exe = os.path.join(ROOT, "dpdk-tcpipstack_amd", "build", "churn_bench")
+    if not os.path.exists(exe):
+        return None
+    out = {}
+    for nflows in (65536, 1 << 20):
+        for permille in (0, 10):
+            r = subprocess.run([exe, str(nflows), "4096", "40", str(permille)], capture_output=True,
+                               text=True, timeout=300)
+            if r.returncode != 0:
+                return {"error": r.stderr.strip()[-300:]}
+            d = json.loads(r.stdout)
+            out[f"tcbs_{nflows + 1}_churn_{permille / 10:g}pct"] = {
+                k: d[k] for k in ("burst_us", "d2h_us", "replay_us", "mpps_with_replay", "stale_per_burst",
+                                  "host_fixups_per_burst", "device_launches_per_burst", "ntcb_end")}
+    return out
+
+
 def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
     """The oracle's faithful restatement of the reference rx path (port), on one host
     core, over a bounded sample of the same workload (first sample_n frames)."""
@@ -430,7 +463,10 @@ def main():
     mpps = total_frames / elapsed_max / 1e6
     k_avg_s = float(np.mean(kern_ms)) / 1e3
     k_med_s = float(np.median(kern_ms)) / 1e3
-    achieved = wl.bytes_per_batch / k_avg_s / 1e9
+    # every rank's mean kernel time; the roofline is quoted on the slowest GPU
+    k_max_s = max_over_ranks(k_avg_s, device)
+    k_min_s = min_over_ranks(k_avg_s, device)
+    achieved = wl.bytes_per_batch / k_max_s / 1e9
     C = {name: int(merged[i]) for i, name in enumerate(rxg.COUNTERS)}
     checks_ok = (C["rx"] == total_frames and C["bytes"] == total_bytes
                  and C["ip_cksum_bad"] == 0 and C["tcp_cksum_bad"] == 0
@@ -465,12 +501,18 @@ def main():
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)
         legs["c5_bidir_copy_inclusive"] = c5_leg(eng, frames, max(3, args.steps // 4), 1, device,
                                                  seed)
+        if rank == 0:
+            legs["replay_churn"] = replay_churn_leg()
         eng.tcb_load(tcb, live)
 
+    # The reference rx path is one lcore (main.c:366-369): its baseline is a host figure,
+    # independent of N.  Rank 0 times it after the timed region at any N; the other ranks
+    # wait at the barrier.
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
         cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds, cores=cores)
+    barrier(device)
 
     traffic, traffic_src = None, None
     tf = TRAFFIC_FILES.get((args.workload, wl.n, args.rec))
@@ -504,8 +546,12 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel_us": round(k_avg_s * 1e6, 2),
-                         "kernel_us_median": round(k_med_s * 1e6, 2),
+                         "kernel_us": round(k_max_s * 1e6, 2),
+                         "kernel_us_rank0_median": round(k_med_s * 1e6, 2),
+                         "kernel_us_min_over_ranks": round(k_min_s * 1e6, 2),
+                         "kernel_us_max_over_ranks": round(k_max_s * 1e6, 2),
+                         "kernel_timing": "HIP events around each launch on its stream; mean "
+                                          "per rank, max over ranks",
                          "algorithmic_bytes_per_launch": wl.bytes_per_batch},
             "cpu_baseline": cpu,
             "counters_ok": bool(checks_ok),

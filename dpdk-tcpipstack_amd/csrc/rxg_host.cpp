@@ -68,6 +68,9 @@ struct rxg_ctx {
     int variant = 0;     // RXG_VARIANT: rx kernel variants (class subsets, ablations)
     int nocount = 0;     // RXG_NOCOUNT: skip the counter reduction
     int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather variants
+    int mirror_rebuild = 0;  // RXG_MIRROR_REBUILD: every mirror sync a full rebuild (round 1)
+    int replay_coarse = 0;   // RXG_REPLAY_COARSE: a write stales every later TCP packet on
+                             // its dport and all fix-ups run on the GPU (round 1)
 
     // tcbs[] writes posted by other threads (rxg_tcb_post), applied by the rx thread
     rxg::MpscRing<rxg_tcb_op> posted{RXG_TCB_QUEUE_CAP};
@@ -96,9 +99,12 @@ struct rxg_ctx {
 
     // mirror changes since the last clear, for rxg_rx_replay's re-classification
     uint64_t gen = 0, burst_gen = 0;
-    std::vector<int32_t> touched;  // dports (old and new) of changed slots
-    bool touched_all = false;      // whole table replaced
-    bool touched_pass2 = false;    // a slot was removed / NULL slots appeared (pass-2 flag)
+    std::vector<TupleKey> touched_keys;  // tuples (old and new) of changed slots
+    std::vector<int32_t> touched_listen; // dports whose LISTENING slots changed (pass 2)
+    bool touched_all = false;            // whole table replaced
+    bool touched_pass2 = false;          // min_null moved (the pass-2 NULL-slot flag)
+    bool replay_on_device = false;       // RXG_CFG_REPLAY_ON_DEVICE
+    uint64_t rp_stats[4] = {0, 0, 0, 0}; // marked, host fix-ups, device fix-ups, launches
 
     // the last burst's device batch (re-classification reads it again)
     const uint8_t *last_frames = nullptr;
@@ -131,10 +137,10 @@ struct rxg_ctx {
     DevBuf d_arp;
     uint32_t arp_mask = 0;
 
-    // replay scratch, kept across calls (no per-burst allocation of the dport map)
-    std::vector<uint8_t> rp_hit = std::vector<uint8_t>(65536, 0);
+    // replay scratch, kept across calls
     std::vector<rxg_rec16> rp_cur;
-    std::vector<uint8_t> rp_stale;
+    std::vector<uint32_t> rp_seq;
+    std::vector<uint64_t> rp_filter;
     const uint64_t *pm_used = nullptr;  // the gather's arena_used (device)
     bool pm_poisoned = false;           // that gather timed out: no payload is handed out
 
@@ -208,6 +214,7 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
         c->grid_tx = cus * (uint32_t)rx_blocks_per_cu(0);
     }
     if (cfg) {
+        c->replay_on_device = (cfg->flags & RXG_CFG_REPLAY_ON_DEVICE) != 0;
         c->max_blocks = cfg->max_blocks;
         if (cfg->zc_bytes) c->zc_bytes = cfg->zc_bytes;
     }
@@ -217,6 +224,9 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     if (const char *v = getenv("RXG_NOCOUNT")) c->nocount = atoi(v);
     if (const char *v = getenv("RXG_PG_VARIANT")) c->pg_variant = atoi(v);
     if (const char *v = getenv("RXG_ZC_BYTES")) c->zc_bytes = strtoull(v, nullptr, 10);
+    if (const char *v = getenv("RXG_MIRROR_REBUILD")) c->mirror_rebuild = atoi(v);
+    if (const char *v = getenv("RXG_REPLAY_COARSE")) c->replay_coarse = atoi(v);
+    if (c->replay_coarse) c->replay_on_device = true;
 #endif
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -293,18 +303,29 @@ extern "C" void *rxg_stream(rxg_ctx *c) { return c ? (void *)c->stream : nullptr
 static hipStream_t pick(rxg_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
 
 // -------------------------------------------------------------------- TCB mirror ---
+// What a write to tcbs[idx] can change for packets of the burst being replayed: pass 1 of
+// packets with the slot's tuple, pass 2 of packets on its dport if it is (or was) LISTENING.
+static void note_slot(rxg_ctx *c, int32_t idx)
+{
+    if (idx >= c->mir.ntcb() || !c->mir.live[idx]) return;
+    const rxg_tcb_tuple &t = c->mir.tcb[idx];
+    TupleKey k;
+    if (tcb_key(t, k)) c->touched_keys.push_back(k);
+    if (t.state == RXG_LISTENING && port_in_range(t.dport)) c->touched_listen.push_back(t.dport);
+}
+
 extern "C" int rxg_tcb_upsert(rxg_ctx *c, int32_t idx, const rxg_tcb_tuple *t)
 {
     if (!c || !t) return fail(-EINVAL, "rxg_tcb_upsert: NULL argument");
     if (t->state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_upsert: state %u", t->state);
     if (idx < 0 || idx >= kMaxTcbs) return fail(-EINVAL, "tcb index %d outside 0..%d", idx, kMaxTcbs - 1);
-    const int32_t old_n = c->mir.ntcb();
-    // a NULL slot appears (slots old_n..idx-1) or disappears (a removed slot reused): the
-    // pass-2 NULL flag of later packets can change
-    if (idx > old_n || (idx < old_n && !c->mir.live[idx])) c->touched_pass2 = true;
-    if (idx < old_n && c->mir.live[idx]) c->touched.push_back(c->mir.tcb[idx].dport);
-    c->touched.push_back(t->dport);
+    const int32_t min_null = c->mir.min_null;
+    note_slot(c, idx);  // the old tuple / listener
     c->mir.upsert(idx, *t);
+    note_slot(c, idx);  // the new ones
+    // NULL slots appearing (old Ntcb .. idx-1) or disappearing (a removed slot reused) move
+    // min_null, the pass-2 NULL-slot flag of later packets
+    if (c->mir.need_rebuild || c->mir.min_null != min_null) c->touched_pass2 = true;
     c->dirty = true;
     c->gen++;
     return 0;
@@ -315,9 +336,10 @@ extern "C" int rxg_tcb_remove(rxg_ctx *c, int32_t idx)
     if (!c) return fail(-EINVAL, "rxg_tcb_remove: ctx NULL");
     if (idx < 0 || idx >= c->mir.ntcb())
         return fail(-EINVAL, "rxg_tcb_remove: index %d outside Ntcb %d", idx, c->mir.ntcb());
-    if (c->mir.live[idx]) c->touched.push_back(c->mir.tcb[idx].dport);
-    c->touched_pass2 = true;
+    const int32_t min_null = c->mir.min_null;
+    note_slot(c, idx);
     c->mir.remove(idx);
+    if (c->mir.need_rebuild || c->mir.min_null != min_null) c->touched_pass2 = true;
     if ((size_t)idx < c->rcv_state.size()) c->rcv_state[idx] = 0;  // FreeWindow
     c->dirty = true;
     c->gen++;
@@ -330,8 +352,9 @@ extern "C" int rxg_tcb_set_state(rxg_ctx *c, int32_t idx, uint8_t state)
     if (state >= RXG_TCP_STATES) return fail(-EINVAL, "rxg_tcb_set_state: state %u", state);
     if (idx < 0 || idx >= c->mir.ntcb() || !c->mir.live[idx])
         return fail(-EINVAL, "rxg_tcb_set_state: index %d is not a live slot", idx);
-    c->touched.push_back(c->mir.tcb[idx].dport);
+    note_slot(c, idx);
     c->mir.set_state(idx, state);
+    note_slot(c, idx);
     c->dirty = true;
     c->gen++;
     return 0;
@@ -401,10 +424,11 @@ static int wait_table_readers(rxg_ctx *c)
     return 0;
 }
 
-// The patches of the TCB and ARP mirrors, in one launch on c->stream.
-static int apply_patches(rxg_ctx *c, std::vector<MirrorPatch> &p)
+// A mirror's patches (at most one per device word), in one launch on c->stream.
+template <typename M>
+static int apply_patches(rxg_ctx *c, M &mirror)
 {
-    dedupe_patches(p);
+    const std::vector<MirrorPatch> &p = mirror.patches;
     if (p.empty()) return 0;
     if (c->patch_ev_set) HIP_OK(hipEventSynchronize(c->patch_ev));  // h_patch free again
     if (p.size() > c->h_patch_cap) {
@@ -424,7 +448,7 @@ static int apply_patches(rxg_ctx *c, std::vector<MirrorPatch> &p)
     c->patch_ev_set = true;
     HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
     c->mirror_ev_set = true;
-    p.clear();
+    mirror.patches_taken();
     return 0;
 }
 
@@ -436,6 +460,7 @@ static int tcb_push(rxg_ctx *c)
     int rc = set_device(c);
     if (rc) return rc;
     TcbMirror &m = c->mir;
+    if (c->mirror_rebuild) m.need_rebuild = true;  // experiment build only
     if (m.need_rebuild) {
         m.rebuild();
         const size_t sb = m.slots.size() * sizeof(Slot), lb = m.listen.size() * sizeof(int32_t);
@@ -453,7 +478,7 @@ static int tcb_push(rxg_ctx *c)
         HIP_OK(hipStreamSynchronize(c->stream));
         HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
         c->mirror_ev_set = true;
-    } else if ((rc = apply_patches(c, m.patches))) {
+    } else if ((rc = apply_patches(c, m))) {
         return rc;
     }
     c->bucket_mask = m.nb - 1;
@@ -513,7 +538,7 @@ static int arp_sync(rxg_ctx *c)
         HIP_OK(hipStreamSynchronize(c->stream));
         HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
         c->mirror_ev_set = true;
-    } else if ((rc = apply_patches(c, a.patches))) {
+    } else if ((rc = apply_patches(c, a))) {
         return rc;
     }
     c->arp_mask = a.ns - 1;
@@ -573,7 +598,8 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
     c->last_stride = b->rec_kind;
     c->pm_n = 0;  // a gather describes the burst it followed
     // the records reflect the mirror as of now: changes are tracked from here (replay)
-    c->touched.clear();
+    c->touched_keys.clear();
+    c->touched_listen.clear();
     c->touched_all = c->touched_pass2 = false;
     c->burst_gen = c->gen;
     LaunchRx L;
@@ -859,6 +885,9 @@ static inline bool rec_is_tcp(const rxg_rec16 &r)
     return r.verdict == RXG_V_DISPATCH || r.verdict == RXG_V_RST_NOPCB || r.verdict == RXG_V_RST_LISTEN_NONSYN;
 }
 
+// A TCP record that findtcb pass 1 did not answer (listener or no TCB): pass 2 decides it.
+static inline bool rec_pass2(const rxg_rec16 &r) { return r.tcb_idx < 0 || (r.flags & RXG_F_LISTEN); }
+
 // Counter contributions of one TCP record (the kernel's definition; only the fields a
 // re-classification can change).
 static void tcp_record_counters(const rxg_rec16 &r, int64_t sign, int64_t *d)
@@ -868,6 +897,40 @@ static void tcp_record_counters(const rxg_rec16 &r, int64_t sign, int64_t *d)
     if (r.verdict == RXG_V_RST_NOPCB) d[RXG_C_NOPCB] += sign;
     if (r.verdict == RXG_V_RST_LISTEN_NONSYN) d[RXG_C_LISTEN_NONSYN] += sign;
     if (r.verdict == RXG_V_DISPATCH) d[RXG_C_DISPATCH] += sign;
+}
+
+// The pass-1 key of a frame of >= 54 bytes, as the kernel forms it: ports = dport << 16 |
+// sport (host order), ipv4_dst as loaded, ipv4_src host order (tcp_tcb.c:134-135,152-155).
+static inline TupleKey frame_key(const uint8_t *f)
+{
+    const uint32_t sport = ((uint32_t)f[34] << 8) | f[35], dport = ((uint32_t)f[36] << 8) | f[37];
+    const uint32_t dst = (uint32_t)f[30] | ((uint32_t)f[31] << 8) | ((uint32_t)f[32] << 16) | ((uint32_t)f[33] << 24);
+    const uint32_t src = ((uint32_t)f[26] << 24) | ((uint32_t)f[27] << 16) | ((uint32_t)f[28] << 8) | f[29];
+    return TupleKey{(dport << 16) | sport, dst, src};
+}
+
+// Re-classify one TCP packet of >= 54 bytes against the table as it stands now, exactly as
+// rx_kernel's classify does (findtcb tcp_tcb.c:127-173, tcp_in.c:47-59), answered from the
+// host index the device mirror is patched from (rxg_mirror.h): the replay's fix-up of a
+// packet whose TCB a handler changed inside the burst.  The fields a
+// table change cannot move (checksums, datalen, flags of the frame) stay as the burst
+// computed them.
+static void host_classify(const rxg_ctx *c, const uint8_t *f, rxg_rec16 &r)
+{
+    const TupleKey k = frame_key(f);
+    uint8_t st = RXG_STATE_NONE;
+    bool lhit = false;
+    const int32_t idx = c->mir.find(k.ports, k.dst, k.src, k.ports >> 16, &st, &lhit);
+    const bool missed = idx < 0 || lhit;  // pass 1 found nothing
+    const bool nslot = missed && c->mir.min_null < (lhit ? idx : c->mir.ntcb());
+    const uint8_t tflags = f[47];
+    r.tcb_idx = idx;
+    r.state = idx >= 0 ? st : (uint8_t)RXG_STATE_NONE;
+    r.verdict = idx < 0 ? RXG_V_RST_NOPCB
+              : (st == RXG_LISTENING && !(tflags & RXG_TCP_FLAG_SYN)) ? RXG_V_RST_LISTEN_NONSYN
+              : RXG_V_DISPATCH;
+    r.flags = (uint8_t)((r.flags & ~(RXG_F_LISTEN | RXG_F_REF_NULLSLOT)) | (lhit ? RXG_F_LISTEN : 0) |
+                        (nslot ? RXG_F_REF_NULLSLOT : 0));
 }
 
 // Re-classify frames sel[0..k) of the last burst against the current mirror (GPU).
@@ -899,6 +962,11 @@ static int reclassify(rxg_ctx *c, const std::vector<uint32_t> &sel, std::vector<
     return 0;
 }
 
+// A bulk change (a reload, a listener change, min_null moving) that leaves more than this
+// many packets of the burst stale re-classifies them in one GPU launch; fewer (and every
+// change to single tuples) are answered from the host index as each packet is reached.
+static constexpr uint32_t kHostReclassifyMax = 256;
+
 // The side effects of etherin.c:21-35, ip.c:26-39 and tcp_in.c:47-72, in packet order.
 extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const *mbufs,
                              void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t stride)
@@ -918,47 +986,118 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
     std::vector<rxg_rec16> &cur = c->rp_cur;
     cur.resize(n);
     for (uint32_t i = 0; i < n; ++i) cur[i] = *(const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
-    std::vector<uint8_t> &stale = c->rp_stale;
-    stale.assign(n, 0);
     int64_t delta[RXG_NCOUNTERS] = {0};
-    std::vector<uint8_t> &hit = c->rp_hit;  // all zero between uses
-    // Mark the TCP packets j >= j0 whose classification the tracked changes can affect,
-    // then forget the changes.  The dport is re-read from the frame (>= 54 bytes unless
-    // RXG_F_TRUNC, which is marked conservatively).
-    auto mark_from = [&](uint32_t j0) {
-        for (int32_t d : c->touched)
-            if (d >= 0 && d <= 0xFFFF) hit[d] = 1;
-        for (uint32_t j = j0; j < n; ++j) {
-            const rxg_rec16 &q = cur[j];
-            if (!rec_is_tcp(q) || stale[j]) continue;
-            bool st = c->touched_all || (q.flags & RXG_F_TRUNC);
-            if (!st) {
-                const uint8_t *g = (const uint8_t *)frames[j];
-                st = hit[((uint32_t)g[36] << 8) | g[37]] != 0;
+
+    // Staleness by write sequence numbers, checked when a packet is reached (its header is
+    // read there anyway; no per-burst index).  Each batch of tracked writes (those of one
+    // handler call, or those made between the burst and the replay) gets a number; a record
+    // computed at number s is stale when a later write touched what it depends on: its tuple
+    // (pass 1, old or new tuple of a written slot), or -- for a packet pass 1 did not answer
+    // -- a LISTENING slot on its dport or the lowest NULL slot (pass 2); any write for a
+    // frame under 54 bytes; everything after a reload.
+    std::vector<uint32_t> &pkt_seq = c->rp_seq;
+    pkt_seq.assign(n, 0u);  // 0 = as the burst classified it
+    uint32_t wseq = 0, any_seq = 0, all_seq = 0, minnull_seq = 0, bulk_seq = 0, scanned_seq = 0;
+    std::unordered_map<TupleKey, uint32_t, TupleKeyHash> key_seq;
+    std::vector<std::pair<int32_t, uint32_t>> listen_seq;  // (dport, seq): rare
+    std::vector<uint64_t> &filt = c->rp_filter;            // 65 536-bit filter of written tuples
+    bool filt_used = false;
+    auto absorb = [&]() {
+        ++wseq;
+        any_seq = wseq;
+        if (c->touched_all) all_seq = bulk_seq = wseq;
+        if (c->touched_pass2) minnull_seq = bulk_seq = wseq;
+        for (const TupleKey &k : c->touched_keys) {
+            key_seq[k] = wseq;
+            const uint32_t h = tuple_hash(k.ports, k.dst, k.src);
+            if (!filt_used) {
+                filt.assign(1024, 0ull);
+                filt_used = true;
             }
-            if (!st && c->touched_pass2) st = q.tcb_idx < 0 || (q.flags & RXG_F_LISTEN);
-            if (st) stale[j] = 1;
+            filt[(h >> 6) & 1023u] |= 1ull << (h & 63u);
         }
-        for (int32_t d : c->touched)
-            if (d >= 0 && d <= 0xFFFF) hit[d] = 0;
-        c->touched.clear();
+        if (c->replay_coarse)  // experiment build only: the round-1 rule, any packet on the dport
+            for (const TupleKey &k : c->touched_keys) listen_seq.emplace_back(-1 - (int32_t)(k.ports >> 16), wseq);
+        for (int32_t d : c->touched_listen) {
+            bool found = false;
+            for (auto &e : listen_seq)
+                if (e.first == d) {
+                    e.second = wseq;
+                    found = true;
+                }
+            if (!found) listen_seq.emplace_back(d, wseq);
+            bulk_seq = wseq;
+        }
+        c->touched_keys.clear();
+        c->touched_listen.clear();
         c->touched_all = c->touched_pass2 = false;
     };
-    if (c->gen != c->burst_gen) mark_from(0);  // changes made between the burst and now
+    auto stale = [&](uint32_t j) -> bool {
+        const rxg_rec16 &q = cur[j];
+        const uint32_t s = pkt_seq[j];
+        if (any_seq <= s || !rec_is_tcp(q)) return false;
+        if (all_seq > s || (q.flags & RXG_F_TRUNC)) return true;
+        const TupleKey k = frame_key((const uint8_t *)frames[j]);
+        if (filt_used) {
+            const uint32_t h = tuple_hash(k.ports, k.dst, k.src);
+            if ((filt[(h >> 6) & 1023u] >> (h & 63u)) & 1ull) {
+                auto it = key_seq.find(k);
+                if (it != key_seq.end() && it->second > s) return true;
+            }
+        }
+        const int32_t d = (int32_t)(k.ports >> 16);
+        if (rec_pass2(q)) {
+            if (minnull_seq > s) return true;
+            for (const auto &e : listen_seq)
+                if (e.first == d && e.second > s) return true;
+        }
+        if (c->replay_coarse)
+            for (const auto &e : listen_seq)
+                if (e.first == -1 - d && e.second > s) return true;
+        return false;
+    };
+    if (c->gen != c->burst_gen) absorb();  // changes made between the burst and now
 
+    std::vector<uint32_t> sel;
+    std::vector<rxg_rec16> fix;
     for (uint32_t i = 0; i < n; ++i) {
-        if (stale[i]) {  // re-classify every stale packet from here on in one launch
-            std::vector<uint32_t> sel;
-            for (uint32_t j = i; j < n; ++j)
-                if (stale[j]) sel.push_back(j);
-            std::vector<rxg_rec16> fix;
-            int rc = reclassify(c, sel, fix);
-            if (rc) return rc;
-            for (size_t k = 0; k < sel.size(); ++k) {
-                tcp_record_counters(cur[sel[k]], -1, delta);
-                tcp_record_counters(fix[k], +1, delta);
-                cur[sel[k]] = fix[k];
-                stale[sel[k]] = 0;
+        if (any_seq > pkt_seq[i] && stale(i)) {
+            ++c->rp_stats[0];
+            const bool trunc = (cur[i].flags & RXG_F_TRUNC) != 0;
+            bool batched = false;
+            if (c->replay_on_device || trunc || bulk_seq > scanned_seq) {
+                // what is stale from here on: one GPU launch if the set is large (a bulk
+                // change), or always on the device path / for a short frame
+                sel.clear();
+                for (uint32_t j = i; j < n; ++j)
+                    if (stale(j)) sel.push_back(j);
+                scanned_seq = wseq;
+                if (c->replay_on_device || trunc || sel.size() > kHostReclassifyMax) {
+                    int rc = reclassify(c, sel, fix);
+                    if (rc) return rc;
+                    for (size_t k = 0; k < sel.size(); ++k) {
+                        tcp_record_counters(cur[sel[k]], -1, delta);
+                        tcp_record_counters(fix[k], +1, delta);
+                        cur[sel[k]] = fix[k];
+                        pkt_seq[sel[k]] = wseq;
+                    }
+                    c->rp_stats[2] += sel.size();
+                    ++c->rp_stats[3];
+                    batched = true;
+                }
+            }
+            if (!batched) {
+                if (c->mir.need_rebuild) {  // a reload / growth inside the replay: index first
+                    int rc = tcb_push(c);
+                    if (rc) return rc;
+                }
+                rxg_rec16 r = cur[i];
+                host_classify(c, (const uint8_t *)frames[i], r);
+                tcp_record_counters(cur[i], -1, delta);
+                tcp_record_counters(r, +1, delta);
+                cur[i] = r;
+                pkt_seq[i] = wseq;
+                ++c->rp_stats[1];
             }
         }
         const rxg_rec16 &r = cur[i];
@@ -1006,7 +1145,7 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
             }
         }
         }
-        if (c->gen != gen_before) mark_from(i + 1);  // the handlers changed the table
+        if (c->gen != gen_before) absorb();  // the handlers changed the table
     }
     c->burst_gen = c->gen;
     bool nz = false;
@@ -1020,6 +1159,13 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         HIP_OK(hipMemcpyAsync(dst, row, sizeof row, hipMemcpyHostToDevice, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
     }
+    return 0;
+}
+
+extern "C" int rxg_replay_stats(rxg_ctx *c, uint64_t out[4])
+{
+    if (!c || !out) return fail(-EINVAL, "rxg_replay_stats: NULL argument");
+    for (int k = 0; k < 4; ++k) out[k] = c->rp_stats[k];
     return 0;
 }
 

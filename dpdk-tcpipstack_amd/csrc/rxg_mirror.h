@@ -64,6 +64,15 @@ struct TupleKeyHash {
 
 inline bool port_in_range(int32_t p) { return p >= 0 && p <= 0xFFFF; }
 
+// The key findtcb pass 1 compares (tcp_tcb.c:152-155); false for a tuple whose int ports lie
+// outside 0..65535, which never equals a packet's u16 ports.
+inline bool tcb_key(const rxg_tcb_tuple &t, TupleKey &k)
+{
+    if (!port_in_range(t.dport) || !port_in_range(t.sport)) return false;
+    k = TupleKey{((uint32_t)t.dport << 16) | (uint32_t)t.sport, t.ipv4_dst, t.ipv4_src};
+    return true;
+}
+
 class TcbMirror {
   public:
     // canonical host copy of tcbs[0..Ntcb)
@@ -76,8 +85,16 @@ class TcbMirror {
     uint32_t nb = 0;
     std::vector<int32_t> listen;  // 65536
     int32_t min_null = INT32_MAX;
-    std::vector<MirrorPatch> patches;  // device writes since the last take_patches()
+    std::vector<MirrorPatch> patches;  // device writes since the last patches_taken(); at
+                                       // most one per device word (a rewrite updates it)
     uint64_t rescans = 0, moves = 0;   // diagnostics (tests)
+
+    // The caller uploaded `patches`: forget them.
+    void patches_taken()
+    {
+        for (const MirrorPatch &q : patches) (q.target == kPatchBucket ? slot_pp[q.index] : listen_pp[q.index]) = kNone;
+        patches.clear();
+    }
 
     int32_t ntcb() const { return (int32_t)tcb.size(); }
 
@@ -90,7 +107,7 @@ class TcbMirror {
         else
             live.assign((size_t)n, 1);
         need_rebuild = true;
-        patches.clear();
+        patches.clear();  // the rebuild resets the pending-patch index
     }
 
     void upsert(int32_t idx, const rxg_tcb_tuple &t)
@@ -177,6 +194,8 @@ class TcbMirror {
             if (!l.second.empty()) listen[l.first] = *l.second.begin();
         need_rebuild = false;
         patches.clear();
+        slot_pp.assign(slots.size(), kNone);
+        listen_pp.assign(65536, kNone);
     }
 
     // ---- pass 1 + pass 2 exactly as the device kernel answers them (tests)
@@ -214,14 +233,10 @@ class TcbMirror {
     };
     std::unordered_map<TupleKey, KeyEntry, TupleKeyHash> keys;
     std::map<int32_t, std::set<int32_t>> listeners;  // dport -> live LISTENING indices
+    static constexpr uint32_t kNone = 0xFFFFFFFFu;
+    std::vector<uint32_t> slot_pp, listen_pp;  // word -> its pending patch, or kNone
 
-    static bool key_of(const rxg_tcb_tuple &t, TupleKey &k)
-    {
-        // a tuple whose int ports are outside 0..65535 never equals a packet's u16 ports
-        if (!port_in_range(t.dport) || !port_in_range(t.sport)) return false;
-        k = TupleKey{((uint32_t)t.dport << 16) | (uint32_t)t.sport, t.ipv4_dst, t.ipv4_src};
-        return true;
-    }
+    static bool key_of(const rxg_tcb_tuple &t, TupleKey &k) { return tcb_key(t, k); }
     static bool same_key(const rxg_tcb_tuple &a, const rxg_tcb_tuple &b)
     {
         return a.dport == b.dport && a.sport == b.sport && a.ipv4_dst == b.ipv4_dst && a.ipv4_src == b.ipv4_src;
@@ -229,14 +244,23 @@ class TcbMirror {
     uint32_t value_of(int32_t idx) const { return (uint32_t)idx | ((uint32_t)tcb[idx].state << kStateShift); }
     uint32_t home(const TupleKey &k) const { return tuple_hash(k.ports, k.dst, k.src) & (nb - 1); }
 
+    void emit(std::vector<uint32_t> &pp, const MirrorPatch &q)
+    {
+        if (pp[q.index] != kNone) {
+            patches[pp[q.index]] = q;  // the word's pending patch takes the new value
+        } else {
+            pp[q.index] = (uint32_t)patches.size();
+            patches.push_back(q);
+        }
+    }
     void emit_slot(uint32_t pos)
     {
         const Slot &e = slots[pos];
-        patches.push_back(MirrorPatch{kPatchBucket, pos, {e.ports, e.dst, e.src, e.val}});
+        emit(slot_pp, MirrorPatch{kPatchBucket, pos, {e.ports, e.dst, e.src, e.val}});
     }
     void emit_listen(uint32_t dport)
     {
-        patches.push_back(MirrorPatch{kPatchListen, dport, {(uint32_t)listen[dport], 0u, 0u, 0u}});
+        emit(listen_pp, MirrorPatch{kPatchListen, dport, {(uint32_t)listen[dport], 0u, 0u, 0u}});
     }
 
     // first free slot from the key's home bucket (load <= 1/2: one exists)
@@ -271,7 +295,6 @@ class TcbMirror {
         }
         if ((uint64_t)(keys.size() + 1) * 2u > (uint64_t)nb * kSlotsPerBucket) {
             need_rebuild = true;  // past load 1/2: rebuilt at twice the size on the next sync
-            patches.clear();
             return;
         }
         const uint32_t pos = place(k, value_of(idx));
@@ -403,7 +426,7 @@ class ArpMirror {
     std::vector<uint32_t> slots;  // ns x {ip, used}
     uint32_t ns = 0;
     bool need_rebuild = true;
-    std::vector<MirrorPatch> patches;
+    std::vector<MirrorPatch> patches;  // one per slot (a slot is written once between loads)
 
     void clear()
     {
@@ -413,6 +436,8 @@ class ArpMirror {
         patches.clear();
     }
 
+    void patches_taken() { patches.clear(); }
+
     // true when ip is new
     bool add(uint32_t ip)
     {
@@ -421,7 +446,6 @@ class ArpMirror {
         if (need_rebuild) return true;
         if ((uint64_t)ips.size() * 2u > ns) {
             need_rebuild = true;
-            patches.clear();
             return true;
         }
         const uint32_t h = insert(ip);
@@ -449,20 +473,5 @@ class ArpMirror {
         return h;
     }
 };
-
-// The last write to each device word wins: keep the final patch per (target, index), in
-// their original order otherwise (the kernel applies them in parallel).
-inline void dedupe_patches(std::vector<MirrorPatch> &p)
-{
-    if (p.size() < 2) return;
-    std::unordered_set<uint64_t> seen;
-    seen.reserve(p.size() * 2);
-    std::vector<MirrorPatch> out;
-    out.reserve(p.size());
-    for (size_t i = p.size(); i-- > 0;)
-        if (seen.insert(((uint64_t)p[i].target << 32) | p[i].index).second) out.push_back(p[i]);
-    std::reverse(out.begin(), out.end());
-    p.swap(out);
-}
 
 }  // namespace rxg

@@ -135,6 +135,7 @@ class HandoffOps(C.Structure):
 
 
 OPS_VERIFY_TCP_CKSUM = 0x1  # rxg_handoff_ops.flags: tcp_in.c:37-41 compiled in
+CFG_REPLAY_ON_DEVICE = 0x1  # rxg_config.flags: every replay fix-up is a GPU re-classify
 
 
 # ------------------------------------------------------------------------- loading ---
@@ -184,6 +185,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_counters_dev": (vp, [vp]),
         "rxg_rx_replay": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, vp, u32, u32]),
         "rxg_ether_in": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, C.c_uint16]),
+        "rxg_replay_stats": (C.c_int, [vp, vp]),
         "rxg_payload_gather_dev": (C.c_int, [vp, C.POINTER(PayloadOut), vp]),
         "rxg_rcv_set": (C.c_int, [vp, i32, u32, u32]),
         "rxg_payload_take": (C.c_int, [vp, i32, u32, u32, C.POINTER(PayloadMsg)]),
@@ -348,9 +350,9 @@ class Engine:
     """One rxg context on one GPU (include/rxg.h: rxg_init .. rxg_fini)."""
 
     def __init__(self, device: int = 0, max_batch: int = 0, max_bytes: int = 0,
-                 max_blocks: int = 0, zc_bytes: int = 0):
+                 max_blocks: int = 0, zc_bytes: int = 0, flags: int = 0):
         load_library()
-        cfg = Config(device, max_batch, max_bytes, 0, max_blocks, zc_bytes)
+        cfg = Config(device, max_batch, max_bytes, flags, max_blocks, zc_bytes)
         ctx = C.c_void_p()
         _check(_lib.rxg_init(C.byref(cfg), C.byref(ctx)), "rxg_init")
         self.ctx = ctx.value
@@ -553,6 +555,11 @@ class Engine:
         rc = _lib.rxg_payload_take(self.ctx, idx, seq & 0xFFFFFFFF, length, C.byref(m))
         _check(min(rc, 0), "rxg_payload_take")
         return rc == 1, int(m.arena_off)
+
+    def replay_stats(self) -> dict:
+        out = np.zeros(4, dtype=np.uint64)
+        _check(_lib.rxg_replay_stats(self.ctx, _ptr(out)), "rxg_replay_stats")
+        return dict(zip(("marked", "host_fixups", "device_fixups", "device_launches"), out.tolist()))
 
     # --- counters
     def counters_reset(self, stream=None):

@@ -170,12 +170,17 @@ typedef struct rxg_config {
     int32_t device;        /* HIP device ordinal (one context per GPU, one rx thread each) */
     uint32_t max_batch;    /* largest n passed to the host-buffer entry points (staging)   */
     uint32_t max_bytes;    /* staging arena bytes for host-buffer entry points            */
-    uint32_t flags;        /* reserved, 0                                                  */
+    uint32_t flags;        /* RXG_CFG_*                                                    */
     uint32_t max_blocks;   /* rx grid cap in workgroups; 0 = one generation of resident
                               workgroups (occupancy).  Any value gives the same records.   */
     uint32_t zc_bytes;     /* rxg_rx_burst: bursts of up to this many staged bytes run
                               zero-copy (kernel reads pinned staging over PCIe); 0 = 64 MiB */
 } rxg_config;
+
+/* rxg_config.flags.  RXG_CFG_REPLAY_ON_DEVICE: rxg_rx_replay re-classifies every packet a
+   handler's tcbs[] write affects with a GPU launch (the default answers small sets from the
+   host index the device mirror is patched from; same records either way). */
+#define RXG_CFG_REPLAY_ON_DEVICE 0x1u
 
 int rxg_abi_version(void);
 const char *rxg_build_info(void);
@@ -369,6 +374,11 @@ typedef struct rxg_handoff_ops {
    burst's or that burst failed after it started (nothing is replayed then). */
 int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
+
+/* Cumulative replay statistics of the context: out[0] packets marked stale by in-burst
+   table writes, out[1] of them re-classified from the host index, out[2] re-classified on
+   the GPU, out[3] GPU re-classify launches. */
+int rxg_replay_stats(rxg_ctx *ctx, uint64_t out[4]);
 
 /* Per-packet form with ether_in's contract (etherin.c:12-37: takes ownership of the mbuf,
    returns 0): a burst of one through the GPU followed by its replay.  For a stack that

@@ -21,3 +21,15 @@ def engine():
     eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20)
     yield eng
     eng.close()
+
+
+@pytest.fixture(scope="session", params=["host", "device"])
+def replay_engine(request):
+    """A context per re-classification mode of rxg_rx_replay: small fix-ups answered from the
+    host index (default) or every fix-up a GPU launch (RXG_CFG_REPLAY_ON_DEVICE).  Both must
+    give the sequential reference's records."""
+    import rxg
+    flags = rxg.CFG_REPLAY_ON_DEVICE if request.param == "device" else 0
+    eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20, flags=flags)
+    yield eng
+    eng.close()

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <set>
 
 #include "rxg_mirror.h"
 
@@ -46,16 +47,18 @@ static void sync_dev(TcbMirror &m, ArpMirror &a, Dev &d, uint64_t &nrebuild, uin
         ++nrebuild;
     } else {
         p.insert(p.end(), m.patches.begin(), m.patches.end());
-        m.patches.clear();
+        m.patches_taken();
     }
     if (a.need_rebuild) {
         a.rebuild();
         d.arp = a.slots;
     } else {
         p.insert(p.end(), a.patches.begin(), a.patches.end());
-        a.patches.clear();
+        a.patches_taken();
     }
-    dedupe_patches(p);
+    // the device kernel applies them in parallel: no two may write the same word
+    std::set<std::pair<uint32_t, uint32_t>> words;
+    for (const MirrorPatch &q : p) CHECK(words.insert({q.target, q.index}).second, "two patches for one word");
     npatch += p.size();
     for (const MirrorPatch &q : p) {
         if (q.target == kPatchBucket)

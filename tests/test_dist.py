@@ -40,10 +40,11 @@ def _worker(rank, world, port, q):
     _, cnt = oracle.rx_batch(arena, off, lens, tcb, live)
     merged = bench.merge_counters(cnt, torch.device("cpu"))
     tmax = bench.max_over_ranks(float(rank + 1) * 0.5, torch.device("cpu"))
+    tmin = bench.min_over_ranks(float(rank + 1) * 0.5, torch.device("cpu"))
     seeds = [bench.shard_seed(0x5EED0001, r) for r in range(world)]
     tsum = bench.sum_over_ranks(len(frames), torch.device("cpu"))
     bench.barrier(torch.device("cpu"))
-    q.put((rank, merged.tolist(), tmax, seeds, tsum))
+    q.put((rank, merged.tolist(), tmax, tmin, seeds, tsum))
     dist.destroy_process_group()
 
 
@@ -66,10 +67,11 @@ def test_two_rank_counter_merge_and_timing():
         arena, off, lens = pktgen.pack_arena(frames)
         tcb, live = pktgen.table_arrays(rows)
         total += oracle.rx_batch(arena, off, lens, tcb, live)[1]
-    for rank, merged, tmax, seeds, tsum in out:
+    for rank, merged, tmax, tmin, seeds, tsum in out:
         assert merged == total.tolist()
         assert tsum == sum(len(_shard(r)[1]) for r in range(world))  # the value's numerator
         assert tmax == pytest.approx(1.0)  # max over ranks of (rank+1)/2
+        assert tmin == pytest.approx(0.5)  # min over ranks (roofline kernel_us spread)
         assert len(set(seeds)) == world     # independent shard per rank
 
 

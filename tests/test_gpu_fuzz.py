@@ -75,7 +75,8 @@ def _post(engine, ops):
 
 
 @pytest.mark.parametrize("seed,arp", [(101, False), (202, False), (303, True)])
-def test_random_bursts_equal_sequential_reference(engine, seed, arp):
+def test_random_bursts_equal_sequential_reference(replay_engine, seed, arp):
+    engine = replay_engine
     """arp: the ARP mirror is on (half the sources known up front); the replay's add_mac
     calls must be the reference's ip_in learns (ip.c:30-32), first sighting in stream
     order, across bursts."""

@@ -125,7 +125,8 @@ def sequential_reference(rows, frames, verify=False, globals_out=None):
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_replay_sequential_equivalence(engine, seed):
+def test_replay_sequential_equivalence(replay_engine, seed):
+    engine = replay_engine
     rows, frames = scenario(seed)
     exp, ecnt, erows = sequential_reference(rows, frames)
     tcb, live = pktgen.table_arrays(rows)
