@@ -142,6 +142,52 @@ def time_workload(eng, wl, steps, warmup, device, stream):
     return elapsed, kern_ms
 
 
+def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20):
+    """C2 (configs[1]: 2^20 x 64 B, 1 flow) as a ring of `nbursts` distinct 2^20-frame bursts
+    in one 1 GiB frame pool (the same working set as the rotating C2 leg, beyond the 256 MB
+    Infinity Cache), classified by ONE launch (rxg_rx_bursts_dev) instead of one launch per
+    burst: the launch ramp and drain are paid once per ring.  Roofline per launch =
+    nbursts x 64 MiB of frame bytes / the launch's event time."""
+    pool = eng.synth(n=n * nbursts, nflows=1, len_a=64, mix=0, seed=seed + 123)
+    tcb, live = rxg.synthetic_tcb_table(1)
+    eng.tcb_load(tcb, live)
+    out = eng.alloc(n * nbursts * 16)
+    bursts = [(pool["off64"].ptr + j * n * 4, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * 16)
+              for j in range(nbursts)]
+    try:
+        for _ in range(warmup):
+            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rxg.REC16)
+        eng.sync()
+        eng.counters_reset()
+        evs = [(eng.event(), eng.event()) for _ in range(steps)]
+        barrier(device)
+        t0 = time.perf_counter()
+        for a, b in evs:
+            eng.record(a)
+            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rxg.REC16)
+            eng.record(b)
+        eng.sync()
+        barrier(device)
+        dt = max_over_ranks(time.perf_counter() - t0, device)
+        k = max_over_ranks(float(np.mean([eng.elapsed_ms(a, b) for a, b in evs])) / 1e3, device)
+        c = merge_counters(eng.counters(), device)
+        frames_all = int(sum_over_ranks(n * nbursts, device)) * steps
+        alg = n * nbursts * 64
+        rec = out.download(rxg.REC16_DTYPE, 4096, offset_bytes=(n * nbursts - 4096) * 16)
+        return {"bursts_per_launch": nbursts, "frames_per_burst": n,
+                "kernel_us_per_launch": round(k * 1e6, 2), "kernel_us_per_burst": round(k * 1e6 / nbursts, 2),
+                "mpps": round(frames_all / dt / 1e6, 2), "gbs": round(frames_all * 64 / dt / 1e9, 2),
+                "roofline_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4), "working_set_GiB": round(alg / 2**30, 3),
+                "counters_ok": bool(int(c[0]) == frames_all and int(c[7]) == 0 and int(c[8]) == 0
+                                    and int(c[13]) == frames_all
+                                    and (rec["verdict"] == rxg.V_DISPATCH).all() and (rec["tcb_idx"] == 1).all())}
+    finally:
+        out.free()
+        for v in pool.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()
+
+
 def copy_inclusive_leg(eng, wl, steps, warmup, device):
     """The path as it runs from host mbufs: pinned H2D of the packed batch (arena +
     descriptors), the rx kernel, D2H of the records; one stream, back to back.  PCIe-bound;
@@ -496,6 +542,7 @@ def main():
                                     and int(c2[7]) == 0 and int(c2[8]) == 0),
             }
             lw.free()
+        legs["c2_64B_1flow_multiburst"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed)
         legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
         legs["tx_generate_dev"] = tx_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)

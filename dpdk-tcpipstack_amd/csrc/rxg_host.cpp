@@ -98,7 +98,7 @@ struct rxg_ctx {
     unsigned long long *counters = nullptr;
 
     // mirror changes since the last clear, for rxg_rx_replay's re-classification
-    uint64_t gen = 0, burst_gen = 0;
+    uint64_t gen = 0;
     std::vector<TupleKey> touched_keys;  // tuples (old and new) of changed slots
     std::vector<int32_t> touched_listen; // dports whose LISTENING slots changed (pass 2)
     bool touched_all = false;            // whole table replaced
@@ -107,6 +107,21 @@ struct rxg_ctx {
     uint64_t rp_stats[4] = {0, 0, 0, 0}; // marked, host fix-ups, device fix-ups, launches
 
     // the last burst's device batch (re-classification reads it again)
+    // The last launch's bursts (one, or several of one frame pool: rxg_rx_bursts_dev) and
+    // the one a replay / gather refers to next (last_off .. last_recs below).
+    struct BurstRef {
+        const uint32_t *off64;
+        const uint16_t *len;
+        uint32_t n;
+        const uint8_t *recs;
+    };
+    std::vector<BurstRef> last_bursts;
+    uint32_t replay_cursor = 0;
+    // writes absorbed by the replays of this launch's earlier bursts (they came after every
+    // burst of the launch was classified)
+    std::vector<TupleKey> launch_keys;
+    std::vector<int32_t> launch_listen;
+    bool launch_all = false, launch_pass2 = false;
     const uint8_t *last_frames = nullptr;
     const uint32_t *last_off = nullptr;
     const uint16_t *last_len = nullptr;
@@ -577,50 +592,90 @@ static DevTable table_view(const rxg_ctx *c)
 }
 
 // ------------------------------------------------------------------------- bursts ---
-extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream)
+static void select_burst(rxg_ctx *c, uint32_t j)
 {
-    if (!c || !b) return fail(-EINVAL, "rxg_rx_burst_dev: NULL argument");
-    if (b->rec_kind != RXG_REC16 && b->rec_kind != RXG_REC48)
-        return fail(-EINVAL, "rxg_rx_burst_dev: rec_kind %u", b->rec_kind);
-    if (b->n && (!b->frames || !b->off64 || !b->len || !b->out))
-        return fail(-EINVAL, "rxg_rx_burst_dev: NULL device pointer");
+    c->replay_cursor = j;
+    const rxg_ctx::BurstRef &b = c->last_bursts[j];
+    c->last_off = b.off64;
+    c->last_len = b.len;
+    c->last_n = b.n;
+    c->last_recs = b.recs;
+    c->pm_n = 0;  // a gather describes the burst it followed
+}
+
+// Classify bursts[0..k) of one frame pool against the mirror as it stands: one launch per
+// kMaxBursts bursts.  The bursts are then replayed in order (rxg_rx_replay).
+static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
+                         void *stream, const char *who)
+{
+    if (rec_kind != RXG_REC16 && rec_kind != RXG_REC48) return fail(-EINVAL, "%s: rec_kind %u", who, rec_kind);
+    if (k && !bursts) return fail(-EINVAL, "%s: NULL burst table", who);
+    bool any = false;
+    for (uint32_t j = 0; j < k; ++j) {
+        if (bursts[j].n && (!bursts[j].off64 || !bursts[j].len || !bursts[j].out))
+            return fail(-EINVAL, "%s: NULL device pointer in burst %u", who, j);
+        any |= bursts[j].n != 0;
+    }
+    if (any && !frames) return fail(-EINVAL, "%s: NULL frame pool", who);
     c->burst_ok = false;
     int rc = set_device(c);
     if (rc) return rc;
     if ((rc = rxg_tcb_sync(c))) return rc;
     if ((rc = arp_sync(c))) return rc;
     c->arp_since_burst.clear();
-    c->last_frames = (const uint8_t *)b->frames;
-    c->last_off = b->off64;
-    c->last_len = b->len;
-    c->last_n = b->n;
-    c->last_recs = (const uint8_t *)b->out;
-    c->last_stride = b->rec_kind;
-    c->pm_n = 0;  // a gather describes the burst it followed
+    c->last_frames = (const uint8_t *)frames;
+    c->last_stride = rec_kind;
+    c->last_bursts.clear();
+    for (uint32_t j = 0; j < k; ++j)
+        c->last_bursts.push_back({bursts[j].off64, bursts[j].len, bursts[j].n, (const uint8_t *)bursts[j].out});
+    if (c->last_bursts.empty()) c->last_bursts.push_back({nullptr, nullptr, 0u, nullptr});
+    select_burst(c, 0);
     // the records reflect the mirror as of now: changes are tracked from here (replay)
     c->touched_keys.clear();
     c->touched_listen.clear();
     c->touched_all = c->touched_pass2 = false;
-    c->burst_gen = c->gen;
-    LaunchRx L;
-    std::memset(&L, 0, sizeof L);
-    L.frames = (const uint8_t *)b->frames;
-    L.off64 = b->off64;
-    L.len = b->len;
-    L.n = b->n;
-    L.mode = (int)b->rec_kind;
-    L.out = (uint8_t *)b->out;
-    L.table = table_view(c);
-    L.counters = c->nocount ? nullptr : c->counters;
-    L.max_blocks = c->max_blocks ? c->max_blocks : (b->rec_kind == RXG_REC48 ? c->grid_rec48 : c->grid_rec16);
-    if (L.max_blocks == 0) L.max_blocks = 1024;
-    L.variant = c->variant;
+    c->launch_keys.clear();
+    c->launch_listen.clear();
+    c->launch_all = c->launch_pass2 = false;
     hipStream_t st = pick(c, stream);
     if ((rc = order_table_reader_before(c, st))) return rc;
-    HIP_OK(launch_rx(L, st));
+    LaunchBurst lb[kMaxBursts];
+    for (uint32_t j0 = 0; j0 < k; j0 += kMaxBursts) {
+        const uint32_t m = std::min(kMaxBursts, k - j0);
+        for (uint32_t j = 0; j < m; ++j)
+            lb[j] = LaunchBurst{bursts[j0 + j].off64, bursts[j0 + j].len, bursts[j0 + j].n, (uint8_t *)bursts[j0 + j].out};
+        LaunchRx L;
+        std::memset(&L, 0, sizeof L);
+        L.frames = (const uint8_t *)frames;
+        L.bursts = lb;
+        L.nbursts = m;
+        L.mode = (int)rec_kind;
+        L.table = table_view(c);
+        L.counters = c->nocount ? nullptr : c->counters;
+        L.max_blocks = c->max_blocks ? c->max_blocks : (rec_kind == RXG_REC48 ? c->grid_rec48 : c->grid_rec16);
+        if (L.max_blocks == 0) L.max_blocks = 1024;
+        L.variant = c->variant;
+        HIP_OK(launch_rx(L, st));
+    }
     if ((rc = order_table_reader_after(c, st))) return rc;
     c->burst_ok = true;
     return 0;
+}
+
+extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream)
+{
+    if (!c || !b) return fail(-EINVAL, "rxg_rx_burst_dev: NULL argument");
+    if (b->n && (!b->frames || !b->off64 || !b->len || !b->out))
+        return fail(-EINVAL, "rxg_rx_burst_dev: NULL device pointer");
+    const rxg_dev_burst one{b->off64, b->len, b->n, 0u, b->out};
+    return launch_bursts(c, b->frames, &one, 1, b->rec_kind, stream, "rxg_rx_burst_dev");
+}
+
+extern "C" int rxg_rx_bursts_dev(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k,
+                                 uint32_t rec_kind, void *stream)
+{
+    if (!c) return fail(-EINVAL, "rxg_rx_bursts_dev: ctx NULL");
+    return launch_bursts(c, frames, bursts, k, rec_kind, stream, "rxg_rx_bursts_dev");
 }
 
 extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *stream)
@@ -630,14 +685,13 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
         return fail(-EINVAL, "rxg_tx_cksum_dev: NULL device pointer");
     int rc = set_device(c);
     if (rc) return rc;
+    const LaunchBurst one{b->off64, b->len, b->n, nullptr};
     LaunchRx L;
     std::memset(&L, 0, sizeof L);
     L.frames = (const uint8_t *)b->frames;
-    L.off64 = b->off64;
-    L.len = b->len;
-    L.n = b->n;
+    L.bursts = &one;
+    L.nbursts = 1;
     L.mode = 0;
-    L.out = nullptr;
     L.counters = nullptr;
     L.max_blocks = c->max_blocks ? c->max_blocks : c->grid_tx;
     if (L.max_blocks == 0) L.max_blocks = 1024;
@@ -943,15 +997,14 @@ static int reclassify(rxg_ctx *c, const std::vector<uint32_t> &sel, std::vector<
     if ((rc = ensure(c->d_fix, sel.size() * sizeof(rxg_rec16)))) return rc;
     if (c->dirty && (rc = tcb_push(c))) return rc;
     HIP_OK(hipMemcpyAsync(c->d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, c->stream));
+    const LaunchBurst one{c->last_off, c->last_len, (uint32_t)sel.size(), (uint8_t *)c->d_fix.p};
     LaunchRx L;
     std::memset(&L, 0, sizeof L);
     L.frames = c->last_frames;
-    L.off64 = c->last_off;
-    L.len = c->last_len;
+    L.bursts = &one;
+    L.nbursts = 1;
     L.sel = (const uint32_t *)c->d_sel.p;
-    L.n = (uint32_t)sel.size();
     L.mode = RXG_REC16;
-    L.out = (uint8_t *)c->d_fix.p;
     L.table = table_view(c);
     L.counters = nullptr;  // corrections go to the host row instead
     L.max_blocks = c->max_blocks ? c->max_blocks : (c->grid_rec16 ? c->grid_rec16 : 1024);
@@ -974,7 +1027,9 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
     if (!c || !ops || (n && (!mbufs || !frames || !recs)))
         return fail(-EINVAL, "rxg_rx_replay: NULL argument");
     if (stride != RXG_REC16 && stride != RXG_REC48) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
-    if (n && c->last_n != n) return fail(-EINVAL, "rxg_rx_replay: n=%u but the last burst had %u frames", n, c->last_n);
+    if (n && c->last_n != n)
+        return fail(-EINVAL, "rxg_rx_replay: n=%u but the burst to replay (%u of the last launch) had %u frames", n,
+                    c->replay_cursor, c->last_n);
     if (n && !c->burst_ok) return fail(-EINVAL, "rxg_rx_replay: the last burst on this context failed");
     // the re-classify launches and the counter correction run on this context's device
     // (a group replays several contexts from one thread, rxg_group.cpp)
@@ -1002,12 +1057,13 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
     std::vector<std::pair<int32_t, uint32_t>> listen_seq;  // (dport, seq): rare
     std::vector<uint64_t> &filt = c->rp_filter;            // 65 536-bit filter of written tuples
     bool filt_used = false;
-    auto absorb = [&]() {
+    auto absorb_lists = [&](const std::vector<TupleKey> &keys, const std::vector<int32_t> &listen, bool all,
+                            bool pass2) {
         ++wseq;
         any_seq = wseq;
-        if (c->touched_all) all_seq = bulk_seq = wseq;
-        if (c->touched_pass2) minnull_seq = bulk_seq = wseq;
-        for (const TupleKey &k : c->touched_keys) {
+        if (all) all_seq = bulk_seq = wseq;
+        if (pass2) minnull_seq = bulk_seq = wseq;
+        for (const TupleKey &k : keys) {
             key_seq[k] = wseq;
             const uint32_t h = tuple_hash(k.ports, k.dst, k.src);
             if (!filt_used) {
@@ -1017,8 +1073,8 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
             filt[(h >> 6) & 1023u] |= 1ull << (h & 63u);
         }
         if (c->replay_coarse)  // experiment build only: the round-1 rule, any packet on the dport
-            for (const TupleKey &k : c->touched_keys) listen_seq.emplace_back(-1 - (int32_t)(k.ports >> 16), wseq);
-        for (int32_t d : c->touched_listen) {
+            for (const TupleKey &k : keys) listen_seq.emplace_back(-1 - (int32_t)(k.ports >> 16), wseq);
+        for (int32_t d : listen) {
             bool found = false;
             for (auto &e : listen_seq)
                 if (e.first == d) {
@@ -1028,6 +1084,15 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
             if (!found) listen_seq.emplace_back(d, wseq);
             bulk_seq = wseq;
         }
+    };
+    // the tracked writes since the last absorb; logged for the launch's later bursts, whose
+    // records were computed before them too
+    auto absorb = [&]() {
+        c->launch_keys.insert(c->launch_keys.end(), c->touched_keys.begin(), c->touched_keys.end());
+        c->launch_listen.insert(c->launch_listen.end(), c->touched_listen.begin(), c->touched_listen.end());
+        c->launch_all |= c->touched_all;
+        c->launch_pass2 |= c->touched_pass2;
+        absorb_lists(c->touched_keys, c->touched_listen, c->touched_all, c->touched_pass2);
         c->touched_keys.clear();
         c->touched_listen.clear();
         c->touched_all = c->touched_pass2 = false;
@@ -1056,7 +1121,11 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
                 if (e.first == -1 - d && e.second > s) return true;
         return false;
     };
-    if (c->gen != c->burst_gen) absorb();  // changes made between the burst and now
+    // writes the replays of this launch's earlier bursts made, then those since
+    if (c->replay_cursor > 0 &&
+        (!c->launch_keys.empty() || !c->launch_listen.empty() || c->launch_all || c->launch_pass2))
+        absorb_lists(c->launch_keys, c->launch_listen, c->launch_all, c->launch_pass2);
+    if (!c->touched_keys.empty() || !c->touched_listen.empty() || c->touched_all || c->touched_pass2) absorb();
 
     std::vector<uint32_t> sel;
     std::vector<rxg_rec16> fix;
@@ -1147,7 +1216,8 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         }
         if (c->gen != gen_before) absorb();  // the handlers changed the table
     }
-    c->burst_gen = c->gen;
+    // the launch's next burst is replayed next (a single burst can be replayed again)
+    if (c->replay_cursor + 1 < c->last_bursts.size()) select_burst(c, c->replay_cursor + 1);
     bool nz = false;
     for (int k = 0; k < RXG_NCOUNTERS; ++k) nz |= delta[k] != 0;
     if (nz) {  // add the corrections to the host row of the counter block

@@ -6,14 +6,22 @@
 
 namespace rxg {
 
-struct LaunchRx {
-    const uint8_t *frames;
+// One launch classifies up to kMaxBursts bursts whose frames share one pool (`frames`):
+// burst k's frame i is at frames + 64 * off64[i], its record at out + i * record size.
+constexpr uint32_t kMaxBursts = 32;
+struct LaunchBurst {
     const uint32_t *off64;
     const uint16_t *len;
-    const uint32_t *sel;   // optional selection list (re-classification), else nullptr
-    uint32_t n;
+    uint32_t n;            // >= 1 (empty bursts are not launched)
+    uint8_t *out;          // records (receive), unused for tx
+};
+
+struct LaunchRx {
+    const uint8_t *frames;
+    const uint32_t *sel;   // optional selection list into burst 0 (re-classification), else nullptr
+    const LaunchBurst *bursts;
+    uint32_t nbursts;      // 1 .. kMaxBursts
     int mode;              // 16 / 48: receive records of that size; 0: tx checksum generate
-    uint8_t *out;
     DevTable table;
     unsigned long long *counters;
     uint32_t max_blocks;   // grid cap (grid-stride over 64-frame slices)

@@ -20,6 +20,7 @@
 //   * Counters: wave-uniform ballot counts, one u64 atomic per counter per workgroup.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <type_traits>
 
 #include "rxg_common.h"
@@ -90,17 +91,109 @@ __device__ __forceinline__ void wcount(WaveCounters &wc, int k, bool pred)
     wc.c[k] += (uint32_t)__popcll(__ballot(pred));
 }
 
-struct RxArgs {
-    const uint8_t *frames;
+// A burst of the launch: its slices are [slice0, slice0 + ceil(n / 64)) of the launch.
+struct RxBurst {
     const uint32_t *off64;
     const uint16_t *len;
-    const uint32_t *sel;  // optional: logical frame i is physical frame sel[i] (re-classify)
-    uint32_t n;
-    uint32_t pad;
     uint8_t *out;
+    uint32_t n;
+    uint32_t slice0;
+};
+
+struct RxArgs {
+    const uint8_t *frames;  // the frame pool every burst's off64 is relative to
+    const uint32_t *sel;    // optional: burst 0's logical frame i is frame sel[i] (re-classify)
+    uint32_t nslices;       // of all bursts
+    uint32_t nbursts;
     DevTable t;
     unsigned long long *counters;
+    RxBurst b[kMaxBursts];
 };
+
+// The burst holding launch slice s (wave-uniform): the last one whose slice0 <= s.
+__device__ __forceinline__ uint32_t burst_of(const RxArgs &a, uint32_t s)
+{
+    uint32_t k = 0;
+    if (a.nbursts > 1) {
+#pragma unroll
+        for (uint32_t step = kMaxBursts / 2; step; step >>= 1)
+            if (k + step < a.nbursts && s >= a.b[k + step].slice0) k += step;
+    }
+    return k;
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// The burst table of a multi-burst launch held in the wave's lanes: lane j keeps burst j's
+// slice0, n and pointers in VGPRs (loaded once per wave), so finding the burst of a slice is
+// one compare + ballot popcount and its fields are v_readlane -- no memory access and no
+// scalar-load wait per lookup.  Single-burst launches (MULTI false) read burst 0 directly.
+template <bool MULTI>
+struct BurstCursor {
+    uint32_t slice0 = 0, n = 0;
+    const uint32_t *off64 = nullptr;
+    const uint16_t *len = nullptr;
+    uint8_t *out = nullptr;
+
+    __device__ __forceinline__ void load(const RxArgs &a, int lane)
+    {
+        if constexpr (MULTI) {
+            const uint32_t j = min((uint32_t)lane, a.nbursts - 1u);
+            slice0 = lane < (int)a.nbursts ? a.b[j].slice0 : 0xFFFFFFFFu;
+            n = a.b[j].n;
+            off64 = a.b[j].off64;
+            len = a.b[j].len;
+            out = a.b[j].out;
+        }
+    }
+    __device__ __forceinline__ uint32_t of(const RxArgs &a, uint32_t s) const
+    {
+        (void)a;
+        if constexpr (!MULTI) return 0u;
+        else return (uint32_t)__popcll(__ballot(s >= slice0)) - 1u;  // slice0 ascending, burst 0 at 0
+    }
+    template <typename T>
+    static __device__ __forceinline__ T *rl_ptr(T *p, uint32_t k)
+    {
+        const uint64_t v = (uint64_t)p;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
+        return (T *)(((uint64_t)hi << 32) | lo);
+    }
+    __device__ __forceinline__ uint32_t slice0_of(const RxArgs &a, uint32_t k) const
+    {
+        if constexpr (!MULTI) return a.b[0].slice0;
+        else return (uint32_t)__builtin_amdgcn_readlane((int)slice0, (int)k);
+    }
+    __device__ __forceinline__ uint32_t n_of(const RxArgs &a, uint32_t k) const
+    {
+        if constexpr (!MULTI) return a.b[0].n;
+        else return (uint32_t)__builtin_amdgcn_readlane((int)n, (int)k);
+    }
+    __device__ __forceinline__ const uint32_t *off64_of(const RxArgs &a, uint32_t k) const
+    {
+        if constexpr (!MULTI) return a.b[0].off64;
+        else return rl_ptr(off64, k);
+    }
+    __device__ __forceinline__ const uint16_t *len_of(const RxArgs &a, uint32_t k) const
+    {
+        if constexpr (!MULTI) return a.b[0].len;
+        else return rl_ptr(len, k);
+    }
+    __device__ __forceinline__ uint8_t *out_of(const RxArgs &a, uint32_t k) const
+    {
+        if constexpr (!MULTI) return a.b[0].out;
+        else return rl_ptr(out, k);
+    }
+};
+
+// Frames in launch slice s (64 except a burst's last slice).
+template <typename BC>
+__device__ __forceinline__ uint32_t slice_frames(const RxArgs &a, uint32_t s, BC &bc)
+{
+    const uint32_t k = bc.of(a, s);
+    return min(64u, bc.n_of(a, k) - (s - bc.slice0_of(a, k)) * 64u);
+}
 
 // One frame's record as classify computes it (16 or 48 bytes, rxg.h rxg_rec16/rxg_rec48).
 struct Rec {
@@ -903,18 +996,20 @@ __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int l
     __builtin_amdgcn_wave_barrier();  // reads done before the LDS is reused
 }
 
-template <bool SEL>
-__device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane, uint32_t &off, uint32_t &len)
+template <bool SEL, typename BC>
+__device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane, uint32_t &off, uint32_t &len, BC &bc)
 {
-    // Unconditional loads of a clamped index (a.n >= 1), not masked here: masking would
-    // consume the load at once, and s_waitcnt retires in order, so the wait would also
-    // drain every older load in flight (the prefetched frames of the small-slice
-    // pipeline).  Callers treat lanes with frame index >= a.n as invalid.
-    const uint32_t f = s * 64u + (uint32_t)lane;
-    const uint32_t fc = min(f, a.n - 1u);
+    // Unconditional loads of a clamped index (every burst has n >= 1), not masked here:
+    // masking would consume the load at once, and s_waitcnt retires in order, so the wait
+    // would also drain every older load in flight (the prefetched frames of the small-slice
+    // pipeline).  Callers treat lanes past their burst's n (slice_frames) as invalid.
+    const uint32_t su = uniform(min(s, a.nslices - 1u));
+    const uint32_t k = bc.of(a, su);
+    const uint32_t f = (su - bc.slice0_of(a, k)) * 64u + (uint32_t)lane;
+    const uint32_t fc = min(f, bc.n_of(a, k) - 1u);
     const uint32_t pf = SEL ? a.sel[fc] : fc;
-    off = a.off64[pf];
-    len = a.len[pf];
+    off = bc.off64_of(a, k)[pf];
+    len = bc.len_of(a, k)[pf];
 }
 
 // Records of a wave's slices are staged in LDS and written out RS slices at a time (and
@@ -925,18 +1020,18 @@ template <int MODE, int RS>
 struct RecRing {
     static constexpr int kQ = MODE / 16;  // uint4 per record
     uint4 (*img)[kQ * 64];                // [RS][kQ * 64]: the slice's records, contiguous
-    uint32_t *base;                       // [RS]: first frame of the slot's slice
+    uint32_t *base;                       // [RS]: the slot's launch slice
     uint32_t n = 0;                       // slots in use (wave-uniform)
 
     // LDS scratch of `bytes` in the free slots (the small-slice transpose, the parked
     // fields of the class path): the slots after the used ones, flushing first if fewer
     // are free.  The slice's own record later goes to the first of them (put), after the
     // scratch has been read.
-    template <bool NTS = false>
-    __device__ __forceinline__ uint32_t *scratch(const RxArgs &a, int lane, int bytes)
+    template <bool NTS = false, typename BC>
+    __device__ __forceinline__ uint32_t *scratch(const RxArgs &a, int lane, int bytes, BC &bc)
     {
         const uint32_t need = (uint32_t)((bytes + kQ * 1024 - 1) / (kQ * 1024));
-        if (n + need > (uint32_t)RS) flush<NTS>(a, lane);
+        if (n + need > (uint32_t)RS) flush<NTS>(a, lane, bc);
         return reinterpret_cast<uint32_t *>(img[n]);
     }
 
@@ -948,7 +1043,7 @@ struct RecRing {
             q[1] = r.q1;
             q[2] = r.q2;
         }
-        if (lane == 0) base[n] = slice * 64u;
+        if (lane == 0) base[n] = slice;
         ++n;
     }
 
@@ -956,19 +1051,22 @@ struct RecRing {
     // stores 1 KiB contiguously.  Records of frames >= n_frames are not written.  NTS:
     // non-temporal stores, used when the small-frame path flushes (C2 0.8-6 % faster across
     // boxes; the 1 500 B path keeps plain stores: 247.5 vs 250.5 us with non-temporal ones).
-    template <bool NTS = false>
-    __device__ __forceinline__ void flush(const RxArgs &a, int lane)
+    template <bool NTS = false, typename BC>
+    __device__ __forceinline__ void flush(const RxArgs &a, int lane, BC &bc)
     {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)base[i]);
-            uint4 *dst = reinterpret_cast<uint4 *>(a.out + (size_t)f0 * MODE);
+            const uint32_t sl = uniform(base[i]);
+            const uint32_t kb = bc.of(a, sl);
+            const uint32_t f0 = (sl - bc.slice0_of(a, kb)) * 64u;  // first frame of the slice in its burst
+            const uint32_t nb = bc.n_of(a, kb);
+            uint4 *dst = reinterpret_cast<uint4 *>(bc.out_of(a, kb) + (size_t)f0 * MODE);
 #pragma unroll
             for (int k = 0; k < kQ; ++k) {
                 const int idx = k * 64 + lane;
-                if (f0 + (uint32_t)(idx / kQ) < a.n) {
+                if (f0 + (uint32_t)(idx / kQ) < nb) {
                     if constexpr (NTS) {
                         typedef unsigned int v4 __attribute__((ext_vector_type(4)));
                         const uint4 q = img[i][idx];
@@ -988,20 +1086,21 @@ struct RecRing {
 
 // One all-small slice s whose frames are in flight in vb[P]; prefetches slice s + nwaves
 // into vb[1-P] when it is all-small too (and returns true: the caller continues the run).
-template <int P, int MODE, int STRIP, bool SEL, int RS>
+template <int P, int MODE, int STRIP, bool SEL, int RS, typename BC>
 __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &s, uint32_t nslices,
                                            uint32_t nwaves, uint32_t &c_off, uint32_t &c_len, uint32_t &n_off,
                                            uint32_t &n_len, uint4 (&vb)[2][4], RecRing<MODE, RS> &ring,
-                                           WaveCounters &wc, Rec &rec, FlowCache &fc, unsigned long long &bytes)
+                                           WaveCounters &wc, Rec &rec, FlowCache &fc, unsigned long long &bytes,
+                                           BC &bc)
 {
     // Issue order (vmcnt retires in order): the TCB probe of this slice, then the next
     // slice's frames, then the descriptors two slices ahead; waiting for the probe leaves
     // both in flight.  (Probe after the frames: the probe's wait drained the prefetch,
     // 64 B / 64 K flows 28.4 us.)
     const uint32_t s1 = s + nwaves;
-    const bool nxt = s1 < nslices && s1 * 64u + 64u <= a.n && __ballot(n_len <= 64u) == ~0ull;
+    const bool nxt = s1 < nslices && slice_frames(a, uniform(s1), bc) == 64u && __ballot(n_len <= 64u) == ~0ull;
     uint32_t d[4][4];
-    uint32_t *sf = ring.template scratch<true>(a, lane, 4096);
+    uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
     transpose_small_slice(vb[P], lane, sf, d);
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
@@ -1010,11 +1109,11 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     const Probe PR = ((STRIP & 2) || cached) ? probe_none() : probe_issue(a, true, F);
     if (nxt) issue_small_slice<true>(a, n_off, n_len, lane, vb[1 - P]);
     uint32_t y_off, y_len;
-    load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len);
+    load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
     classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PR, wc, rec, fc, cached);
     bytes += c_len;
     if (!(STRIP & 4)) {
-        if (ring.n == RS) ring.template flush<true>(a, lane);
+        if (ring.n == RS) ring.template flush<true>(a, lane, bc);
         ring.put(s, lane, rec);
     }
     s = s1;
@@ -1023,7 +1122,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     return nxt;
 }
 
-template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11>
+template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false>
 __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 {
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -1041,7 +1140,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     const int wid = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
     const uint32_t nwaves = gridDim.x * 4u;
-    const uint32_t nslices = (a.n + 63u) >> 6;
+    const uint32_t nslices = a.nslices;
 
     WaveCounters wc;
 #pragma unroll
@@ -1057,11 +1156,13 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     // loads are always in flight while slice s is processed.
     uint32_t s = wave;
     uint32_t c_off = 0, c_len = 0, n_off = 0, n_len = 0;
-    load_desc<SEL>(a, s, lane, c_off, c_len);
-    load_desc<SEL>(a, s + nwaves, lane, n_off, n_len);
+    BurstCursor<MULTI> bc;
+    bc.load(a, lane);
+    load_desc<SEL>(a, s, lane, c_off, c_len, bc);
+    load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
     while (s < nslices) {
         const uint32_t f = s * 64u + (uint32_t)lane;
-        const bool valid = f < a.n;
+        const bool valid = (uint32_t)lane < slice_frames(a, uniform(s), bc);
         const uint32_t off = c_off, len = valid ? c_len : 0u;
         const int cls = valid ? size_class(len) : 9;
         if constexpr (MODE != 0 && (CMASK & 1)) {
@@ -1077,17 +1178,17 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
                 issue_small_slice<true>(a, c_off, c_len, lane, vb[0]);
                 for (;;) {
                     if (!small_step<0, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
-                                                             n_len, vb, ring, wc, rec, fcache, bytes))
+                                                             n_len, vb, ring, wc, rec, fcache, bytes, bc))
                         break;
                     if (!small_step<1, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
-                                                             n_len, vb, ring, wc, rec, fcache, bytes))
+                                                             n_len, vb, ring, wc, rec, fcache, bytes, bc))
                         break;
                 }
                 continue;
             }
         }
         bytes += len;
-        uint32_t *sf = MODE == 0 ? nullptr : ring.scratch(a, lane, NF * 256);
+        uint32_t *sf = MODE == 0 ? nullptr : ring.scratch(a, lane, NF * 256, bc);
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
@@ -1108,15 +1209,15 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
             classify_store<MODE, STRIP>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc, rec, fcache);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
             if (!(STRIP & 4)) {
-                if (ring.n == RS) ring.flush(a, lane);
+                if (ring.n == RS) ring.flush(a, lane, bc);
                 ring.put(s, lane, rec);
             }
         }
         s += nwaves;
         c_off = n_off; c_len = n_len;
-        load_desc<SEL>(a, s + nwaves, lane, n_off, n_len);
+        load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
     }
-    if constexpr (MODE != 0) ring.flush(a, lane);
+    if constexpr (MODE != 0) ring.flush(a, lane, bc);
 
     if (a.counters == nullptr) return;
     // wave -> workgroup -> one atomic per counter
@@ -1255,17 +1356,26 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthArgs s)
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
 {
     RxArgs a;
+    std::memset(&a, 0, sizeof a);
     a.frames = L.frames;
-    a.off64 = L.off64;
-    a.len = L.len;
     a.sel = L.sel;
-    a.n = L.n;
-    a.pad = 0;
-    a.out = L.out;
     a.t = L.table;
     a.counters = L.counters;
-    if (L.n == 0) return hipSuccess;
-    const uint32_t nslices = (L.n + 63u) / 64u;
+    if (L.nbursts > kMaxBursts) return hipErrorInvalidValue;
+    uint32_t nslices = 0;
+    for (uint32_t k = 0; k < L.nbursts; ++k) {
+        const LaunchBurst &B = L.bursts[k];
+        if (B.n == 0) continue;
+        RxBurst &r = a.b[a.nbursts++];
+        r.off64 = B.off64;
+        r.len = B.len;
+        r.out = B.out;
+        r.n = B.n;
+        r.slice0 = nslices;
+        nslices += (B.n + 63u) / 64u;
+    }
+    a.nslices = nslices;
+    if (nslices == 0) return hipSuccess;
     uint32_t blocks = (nslices + 3u) / 4u;
     if (blocks > L.max_blocks) blocks = L.max_blocks;
     // production kernels use non-temporal loads for the >256 B classes (measured +5 %
@@ -1287,13 +1397,23 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 8: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
         case 9: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         case 10: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 8>), dim3(blocks), dim3(256), 0, st, a); break;
-        default: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
+        default:
+            if (a.nbursts > 1)
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
 #else
-        hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
+        if (a.nbursts > 1)
+            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
 #endif
     } else if (L.mode == 48) {
-        hipLaunchKernelGGL((rx_kernel<48, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
+        if (a.nbursts > 1)
+            hipLaunchKernelGGL((rx_kernel<48, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((rx_kernel<48, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     } else {
         hipLaunchKernelGGL((rx_kernel<0, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     }

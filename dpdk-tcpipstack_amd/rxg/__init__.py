@@ -89,6 +89,12 @@ class DevBatch(C.Structure):
                 ("n", C.c_uint32), ("rec_kind", C.c_uint32), ("out", C.c_void_p)]
 
 
+class DevBurst(C.Structure):
+    """rxg_dev_burst: one burst of a multi-burst launch (rxg_rx_bursts_dev)."""
+    _fields_ = [("off64", C.c_void_p), ("len", C.c_void_p), ("n", C.c_uint32), ("pad", C.c_uint32),
+                ("out", C.c_void_p)]
+
+
 class DevTxBatch(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("off64", C.c_void_p), ("len", C.c_void_p),
                 ("n", C.c_uint32), ("pad", C.c_uint32)]
@@ -178,6 +184,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_arp_count": (i32, [vp]),
         "rxg_arp_disable": (C.c_int, [vp]),
         "rxg_rx_burst_dev": (C.c_int, [vp, C.POINTER(DevBatch), vp]),
+        "rxg_rx_bursts_dev": (C.c_int, [vp, vp, vp, u32, u32, vp]),
         "rxg_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
         "rxg_tx_cksum_dev": (C.c_int, [vp, C.POINTER(DevTxBatch), vp]),
         "rxg_counters_reset": (C.c_int, [vp, vp]),
@@ -477,6 +484,12 @@ class Engine:
                      rec_kind: int = REC16, stream=None):
         b = DevBatch(frames, off64, lens, n, rec_kind, out)
         _check(_lib.rxg_rx_burst_dev(self.ctx, C.byref(b), stream), "rxg_rx_burst_dev")
+
+    def rx_bursts_dev(self, frames: int, bursts, rec_kind: int = REC16, stream=None):
+        """bursts: [(off64 ptr, len ptr, n, out ptr), ...] of one frame pool, one launch."""
+        arr = (DevBurst * max(len(bursts), 1))(*[DevBurst(o, l, n, 0, out) for o, l, n, out in bursts])
+        _check(_lib.rxg_rx_bursts_dev(self.ctx, frames, arr, len(bursts), rec_kind, stream),
+               "rxg_rx_bursts_dev")
 
     def tx_cksum_dev(self, frames: int, off64: int, lens: int, n: int, stream=None):
         b = DevTxBatch(frames, off64, lens, n, 0)

@@ -283,6 +283,24 @@ typedef struct rxg_dev_batch {
    resident in HBM.  Asynchronous on `stream`. */
 int rxg_rx_burst_dev(rxg_ctx *ctx, const rxg_dev_batch *b, void *stream);
 
+/* Several bursts of one frame pool in one launch (e.g. the bursts of several rx queues, or a
+   ring of bursts): burst j's frame i is at frames + 64*bursts[j].off64[i] (same readability
+   rules as rxg_dev_batch), its record at bursts[j].out + i * rec_kind.  Every burst is
+   classified against the mirror as it stands at the call, exactly as k rxg_rx_burst_dev
+   calls with no mirror writes between them; one launch (per 32 bursts) instead of k, so the
+   launch ramp is paid once.  The bursts are then replayed in order, one rxg_rx_replay call
+   each (a replay sees the tcbs[] writes of the earlier bursts' replays), and
+   rxg_payload_gather_dev gathers the burst to be replayed next.  Asynchronous on `stream`. */
+typedef struct rxg_dev_burst {
+    const uint32_t *off64;  /* dev, n entries, in 64-byte units of the frame pool */
+    const uint16_t *len;    /* dev, n entries */
+    uint32_t n;
+    uint32_t pad;
+    void *out;              /* dev, n records */
+} rxg_dev_burst;
+int rxg_rx_bursts_dev(rxg_ctx *ctx, const void *frames, const rxg_dev_burst *bursts, uint32_t k,
+                      uint32_t rec_kind, void *stream);
+
 /* DPDK-compatible host packet view: frame = (char*)buf_addr + data_off, data_len bytes
    (struct rte_mbuf fields of the same names). */
 typedef struct rxg_pkt_view {
@@ -370,8 +388,10 @@ typedef struct rxg_handoff_ops {
    changed slot; any packet that reached findtcb pass 2 after a slot was removed or NULL
    slots appeared) is re-classified on the GPU against the updated table before it is
    replayed, and the counters are corrected.  The composition rxg_rx_burst + rxg_rx_replay
-   therefore equals `for (i<n) ether_in(mbufs[i])`.  -EINVAL when n differs from the last
-   burst's or that burst failed after it started (nothing is replayed then). */
+   therefore equals `for (i<n) ether_in(mbufs[i])`.  After rxg_rx_bursts_dev the launch's
+   bursts are replayed in order, one call each, and their composition equals ether_in over
+   their concatenation.  -EINVAL when n differs from the burst to be replayed or the launch
+   failed after it started (nothing is replayed then). */
 int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
 
