@@ -34,7 +34,20 @@ METRIC = "Mpps + GB/s rx parse+checksum+classify, device-resident, 64B & 1500B f
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Per-launch HBM traffic from the committed rocprofv3 PMC passes of this same command
 # (scripts/gpu_check.sh pmc; scripts/pmc_traffic.py applies the gfx950 FETCH_SIZE x2 fix).
-TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r01/c3/traffic.json"}
+TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.json",
+                 ("c2_64B_1flow", 1 << 20, 16): "profiles/r02/c2/traffic.json",
+                 ("c4_imix_64Kflows", 1 << 20, 16): "profiles/r02/c4/traffic.json",
+                 ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r02/c2multi/traffic.json"}
+
+
+def traffic_of(name, n, rec):
+    """Per-launch HBM bytes of the committed PMC passes of this workload (scripts/gpu_prof.sh),
+    or None."""
+    tf = TRAFFIC_FILES.get((name, n, rec))
+    if tf and os.path.exists(os.path.join(ROOT, tf)):
+        with open(os.path.join(ROOT, tf)) as fh:
+            return json.load(fh)["hbm_bytes_per_launch"], tf
+    return None, None
 WORKLOADS = {
     # name: (frame_len, flows, mix, rotating copies)
     "c3_1500B_1Kflows": (1500, 1000, 0, 1),
@@ -175,6 +188,8 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20):
         alg = n * nbursts * 64
         rec = out.download(rxg.REC16_DTYPE, 4096, offset_bytes=(n * nbursts - 4096) * 16)
         return {"bursts_per_launch": nbursts, "frames_per_burst": n,
+                "traffic_bytes_per_launch": traffic_of("c2_64B_1flow_multiburst", n, 16)[0],
+                "algorithmic_bytes_per_launch": alg,
                 "kernel_us_per_launch": round(k * 1e6, 2), "kernel_us_per_burst": round(k * 1e6 / nbursts, 2),
                 "mpps": round(frames_all / dt / 1e6, 2), "gbs": round(frames_all * 64 / dt / 1e9, 2),
                 "roofline_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4), "working_set_GiB": round(alg / 2**30, 3),
@@ -540,6 +555,8 @@ def main():
                 "working_set_GiB": round(lw.copies * (lw.batches[0]["arena_bytes"]) / 2**30, 3),
                 "counters_ok": bool(int(c2[0]) == ln
                                     and int(c2[7]) == 0 and int(c2[8]) == 0),
+                "traffic_bytes_per_launch": traffic_of(name, lw.n, args.rec)[0],
+                "algorithmic_bytes_per_launch": lw.bytes_per_batch,
             }
             lw.free()
         legs["c2_64B_1flow_multiburst"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed)
@@ -561,12 +578,7 @@ def main():
         cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds, cores=cores)
     barrier(device)
 
-    traffic, traffic_src = None, None
-    tf = TRAFFIC_FILES.get((args.workload, wl.n, args.rec))
-    if tf and os.path.exists(os.path.join(ROOT, tf)):
-        with open(os.path.join(ROOT, tf)) as fh:
-            traffic = json.load(fh)["hbm_bytes_per_launch"]
-        traffic_src = tf
+    traffic, traffic_src = traffic_of(args.workload, wl.n, args.rec)
 
     if rank == 0:
         line = {
