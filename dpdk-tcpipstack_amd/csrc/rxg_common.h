@@ -26,7 +26,10 @@ namespace rxg {
 //   min_null: lowest removed slot index (pass 2 would dereference NULL there).
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-constexpr int kSlotsPerBucket = 4;
+#ifndef RXG_SLOTS_PER_BUCKET
+#define RXG_SLOTS_PER_BUCKET 4
+#endif
+constexpr int kSlotsPerBucket = RXG_SLOTS_PER_BUCKET;
 constexpr uint32_t kIdxMask = 0x00FFFFFFu;
 constexpr int kStateShift = 24;
 constexpr int32_t kMaxTcbs = 0x00FFFFFF;  // indices 0 .. kMaxTcbs-1

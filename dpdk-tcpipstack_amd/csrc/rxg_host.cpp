@@ -241,6 +241,7 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     if (const char *v = getenv("RXG_ZC_BYTES")) c->zc_bytes = strtoull(v, nullptr, 10);
     if (const char *v = getenv("RXG_MIRROR_REBUILD")) c->mirror_rebuild = atoi(v);
     if (const char *v = getenv("RXG_REPLAY_COARSE")) c->replay_coarse = atoi(v);
+    if (const char *v = getenv("RXG_MIRROR_LOAD_PCT")) c->mir.max_load_pct = (uint32_t)atoi(v);
     if (c->replay_coarse) c->replay_on_device = true;
 #endif
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

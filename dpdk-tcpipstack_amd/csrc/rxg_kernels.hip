@@ -742,10 +742,11 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
 // First bucket of the exact-tuple probe, loaded early so that several frames' probes of
 // one lane are in flight together.
 struct Probe {
-    uint4 s0, s1, s2, s3;
+    uint4 s[kSlotsPerBucket];
     uint32_t hb;
 };
 
+template <int STRIP = 0>
 __device__ __forceinline__ Probe probe_issue(const RxArgs &a, bool valid, const Fields &F)
 {
     Probe P;
@@ -754,7 +755,14 @@ __device__ __forceinline__ Probe probe_issue(const RxArgs &a, bool valid, const 
     P.hb = tuple_hash(F.ports, F.dst, bswap32(F.src)) & a.t.bucket_mask;
     // always a valid bucket: load unconditionally (see load_chunks), use only for TCP
     const uint4 *b = a.t.buckets + (size_t)P.hb * kSlotsPerBucket;
-    P.s0 = b[0]; P.s1 = b[1]; P.s2 = b[2]; P.s3 = b[3];
+    if constexpr (STRIP & 16) {  // experiment build only (timing): one slot per lane
+        P.s[0] = b[0];
+#pragma unroll
+        for (int k = 1; k < kSlotsPerBucket; ++k) P.s[k] = make_uint4(0u, 0u, 0u, kEmpty);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kSlotsPerBucket; ++k) P.s[k] = b[k];
+    }
     (void)is_tcp;
     return P;
 }
@@ -773,7 +781,8 @@ constexpr uint32_t kFcValid = 0x80000000u;
 __device__ __forceinline__ Probe probe_none()
 {
     Probe P;
-    P.s0 = P.s1 = P.s2 = P.s3 = make_uint4(0u, 0u, 0u, kEmpty);
+#pragma unroll
+    for (int k = 0; k < kSlotsPerBucket; ++k) P.s[k] = make_uint4(0u, 0u, 0u, kEmpty);
     P.hb = 0;
     return P;
 }
@@ -796,7 +805,7 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = valid && et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
-    const Probe P = ((STRIP & 2) || cached) ? probe_none() : probe_issue(a, valid, F);
+    const Probe P = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, valid, F);
     classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr, fc, cached);
 }
 
@@ -843,23 +852,28 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
         }
     } else if (is_tcp && !(STRIP & 2)) {
         uint32_t hb = P.hb;
-        uint4 s0 = P.s0, s1 = P.s1, s2 = P.s2, s3 = P.s3;
+        uint4 sl[kSlotsPerBucket];
+#pragma unroll
+        for (int k = 0; k < kSlotsPerBucket; ++k) sl[k] = P.s[k];
         for (uint32_t probe = 0; probe <= a.t.bucket_mask; ++probe) {
             if (probe) {
                 const uint4 *b = a.t.buckets + (size_t)hb * kSlotsPerBucket;
-                s0 = b[0]; s1 = b[1]; s2 = b[2]; s3 = b[3];
+#pragma unroll
+                for (int k = 0; k < kSlotsPerBucket; ++k) sl[k] = b[k];
             }
             uint32_t v = kEmpty;
-            if (s0.x == ports && s0.y == dst_raw && s0.z == src_host && s0.w != kEmpty) v = s0.w;
-            if (s1.x == ports && s1.y == dst_raw && s1.z == src_host && s1.w != kEmpty) v = s1.w;
-            if (s2.x == ports && s2.y == dst_raw && s2.z == src_host && s2.w != kEmpty) v = s2.w;
-            if (s3.x == ports && s3.y == dst_raw && s3.z == src_host && s3.w != kEmpty) v = s3.w;
+            bool empty = false;
+#pragma unroll
+            for (int k = 0; k < kSlotsPerBucket; ++k) {
+                if (sl[k].x == ports && sl[k].y == dst_raw && sl[k].z == src_host && sl[k].w != kEmpty) v = sl[k].w;
+                empty |= sl[k].w == kEmpty;
+            }
             if (v != kEmpty) {
                 idx = (int32_t)(v & kIdxMask);
                 st = v >> kStateShift;
                 break;
             }
-            if (s0.w == kEmpty || s1.w == kEmpty || s2.w == kEmpty || s3.w == kEmpty) break;
+            if (empty) break;
             hb = (hb + 1u) & a.t.bucket_mask;
         }
         if (idx < 0) {  // pass 2: first LISTENING slot on dport (its state is LISTENING)
@@ -1106,7 +1120,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
-    const Probe PR = ((STRIP & 2) || cached) ? probe_none() : probe_issue(a, true, F);
+    const Probe PR = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, true, F);
     if (nxt) issue_small_slice<true>(a, n_off, n_len, lane, vb[1 - P]);
     uint32_t y_off, y_len;
     load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
@@ -1397,6 +1411,11 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 8: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
         case 9: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         case 10: hipLaunchKernelGGL((rx_kernel<16, 0x20, true, 8>), dim3(blocks), dim3(256), 0, st, a); break;
+        // all classes: 11 no TCB probe, 12 no record store, 13 no phase B (where C4's time goes)
+        case 11: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 2>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 12: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 13: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 8>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 14: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 16>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
             if (a.nbursts > 1)
                 hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);

@@ -87,6 +87,7 @@ class TcbMirror {
     int32_t min_null = INT32_MAX;
     std::vector<MirrorPatch> patches;  // device writes since the last patches_taken(); at
                                        // most one per device word (a rewrite updates it)
+    uint32_t max_load_pct = 50;        // keys per slot, percent: rebuilt past it
     uint64_t rescans = 0, moves = 0;   // diagnostics (tests)
 
     // The caller uploaded `patches`: forget them.
@@ -185,7 +186,7 @@ class TcbMirror {
             if (t.state == RXG_LISTENING && port_in_range(t.dport)) listeners[t.dport].insert(i);
         }
         nb = 1;
-        while ((uint64_t)nb * kSlotsPerBucket < (uint64_t)k.size() * 2u) nb <<= 1;
+        while ((uint64_t)nb * kSlotsPerBucket * max_load_pct < (uint64_t)k.size() * 100u) nb <<= 1;
         slots.assign((size_t)nb * kSlotsPerBucket, Slot{0u, 0u, 0u, kEmpty});
         for (auto &kv : k) kv.second.pos = place(kv.first, value_of(kv.second.min_idx));
         keys.swap(k);
@@ -293,7 +294,7 @@ class TcbMirror {
             }
             return;
         }
-        if ((uint64_t)(keys.size() + 1) * 2u > (uint64_t)nb * kSlotsPerBucket) {
+        if ((uint64_t)(keys.size() + 1) * 100u > (uint64_t)nb * kSlotsPerBucket * max_load_pct) {
             need_rebuild = true;  // past load 1/2: rebuilt at twice the size on the next sync
             return;
         }

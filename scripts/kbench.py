@@ -58,6 +58,8 @@ def main():
         os.environ["RXG_VARIANT"] = parts[0]
         os.environ["RXG_MAX_BLOCKS"] = parts[1]
         os.environ["RXG_NOCOUNT"] = "1" if (len(parts) > 2 and parts[2] == "nc") else "0"
+        # 5th field: the mirror's load limit in percent (RXG_MIRROR_LOAD_PCT)
+        os.environ["RXG_MIRROR_LOAD_PCT"] = parts[4] if len(parts) > 4 and parts[4] else "50"
         lib = main_lib
         if len(parts) > 3 and parts[3]:
             rxg._lib = None
