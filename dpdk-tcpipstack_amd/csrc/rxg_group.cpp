@@ -10,10 +10,13 @@
 // the group is sequentially equivalent to ether_in over the whole burst.
 //
 // Built on the public C ABI only (include/rxg.h).
+#include <rccl/rccl.h>
+
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -31,6 +34,13 @@ struct rxg_group {
     // posts from other threads: one queue for the group, so every member applies them in
     // the same (claim) order and the replicas stay identical
     rxg::MpscRing<rxg_tcb_op> posted{RXG_TCB_QUEUE_CAP};
+    // counter merge: one RCCL communicator per member (ncclCommInitAll) when the members are
+    // distinct GPUs, set up at the first rxg_group_counters_read; the all-reduce writes into
+    // `merged` (one counter block per member), never into the members' own blocks
+    std::vector<int32_t> devices;
+    int rccl = -1;  // -1 not tried, 0 host sum (members share a GPU), 1 RCCL
+    std::vector<ncclComm_t> comms;
+    std::vector<void *> merged;
 };
 
 namespace {
@@ -102,6 +112,7 @@ extern "C" int rxg_group_init(const int32_t *devices, uint32_t ndev, const rxg_c
             return rc;
         }
         g->m.push_back(ctx);
+        g->devices.push_back(devices[i]);
     }
     *out = g;
     return 0;
@@ -110,6 +121,9 @@ extern "C" int rxg_group_init(const int32_t *devices, uint32_t ndev, const rxg_c
 extern "C" int rxg_group_fini(rxg_group *g)
 {
     if (!g) return 0;
+    for (ncclComm_t c : g->comms) (void)ncclCommDestroy(c);
+    for (size_t i = 0; i < g->merged.size(); ++i)
+        if (g->merged[i]) (void)rxg_dev_free(g->m[i], g->merged[i]);
     for (rxg_ctx *c : g->m) rxg_fini(c);
     delete g;
     return 0;
@@ -296,17 +310,77 @@ extern "C" int rxg_group_counters_reset(rxg_group *g)
     });
 }
 
+static constexpr size_t kCounterWords = (size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS;
+
+// One communicator per member over the members' devices; only for distinct GPUs (RCCL
+// takes one rank per device).
+static int rccl_setup(rxg_group *g)
+{
+    if (g->rccl >= 0) return 0;
+    g->rccl = 0;
+    const std::set<int32_t> distinct(g->devices.begin(), g->devices.end());
+    if (distinct.size() != g->devices.size()) return 0;  // members share a GPU: host sum
+    const int n = (int)g->m.size();
+    g->merged.assign((size_t)n, nullptr);
+    for (int i = 0; i < n; ++i)
+        if (rxg_dev_alloc(g->m[(size_t)i], kCounterWords * sizeof(uint64_t), &g->merged[(size_t)i]))
+            return gfail(-ENOMEM, "rxg_group_counters_read: member %d: %s", i, rxg_last_error());
+    g->comms.assign((size_t)n, nullptr);
+    const ncclResult_t r = ncclCommInitAll(g->comms.data(), n, g->devices.data());
+    if (r != ncclSuccess) {
+        g->comms.clear();
+        return gfail(-EIO, "rxg_group_counters_read: ncclCommInitAll: %s", ncclGetErrorString(r));
+    }
+    g->rccl = 1;
+    return 0;
+}
+
+// The members' counters summed.  Distinct GPUs: an RCCL all-reduce (sum, uint64) of the
+// members' counter blocks over xGMI into `merged`, then member 0's merged block is read
+// (the one collective of the design).  Members sharing a GPU: summed on
+// the host.
 extern "C" int rxg_group_counters_read(rxg_group *g, uint64_t *out)
 {
     if (!g || !out) return gfail(-EINVAL, "rxg_group_counters_read: NULL argument");
+    int rc = rccl_setup(g);
+    if (rc) return rc;
     std::memset(out, 0, sizeof(uint64_t) * RXG_NCOUNTERS);
+    if (g->rccl == 1) {
+        const size_t n = g->m.size();
+        for (size_t i = 0; i < n; ++i)  // every burst's counter adds are done (stream order)
+            if ((rc = rxg_sync(g->m[i]))) return gfail(rc, "member %zu: %s", i, rxg_last_error());
+        if (ncclGroupStart() != ncclSuccess) return gfail(-EIO, "rxg_group_counters_read: ncclGroupStart");
+        for (size_t i = 0; i < n; ++i) {
+            const ncclResult_t r = ncclAllReduce(rxg_counters_dev(g->m[i]), g->merged[i], kCounterWords, ncclUint64,
+                                                 ncclSum, g->comms[i], (hipStream_t)rxg_stream(g->m[i]));
+            if (r != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return gfail(-EIO, "rxg_group_counters_read: ncclAllReduce: %s", ncclGetErrorString(r));
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return gfail(-EIO, "rxg_group_counters_read: ncclGroupEnd");
+        std::vector<uint64_t> rows(kCounterWords);
+        if ((rc = rxg_memcpy_d2h(g->m[0], rows.data(), g->merged[0], kCounterWords * sizeof(uint64_t), nullptr)) ||
+            (rc = rxg_sync(g->m[0])))
+            return gfail(rc, "member 0: %s", rxg_last_error());
+        for (size_t k = 0; k < RXG_NCOUNTERS; ++k)
+            for (size_t r = 0; r < RXG_COUNTER_ROWS; ++r) out[k] += rows[r * RXG_NCOUNTERS + k];
+        return 0;
+    }
     for (rxg_ctx *c : g->m) {
         uint64_t v[RXG_NCOUNTERS];
-        const int rc = rxg_counters_read(c, v);
+        rc = rxg_counters_read(c, v);
         if (rc) return rc;
         for (int k = 0; k < RXG_NCOUNTERS; ++k) out[k] += v[k];
     }
     return 0;
+}
+
+extern "C" int rxg_group_counters_rccl(rxg_group *g)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_counters_rccl: group NULL");
+    const int rc = rccl_setup(g);
+    return rc ? rc : g->rccl;
 }
 
 extern "C" const char *rxg_group_last_error(void) { return g_err; }

@@ -233,6 +233,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_group_replaying": (i32, [vp]),
         "rxg_group_counters_reset": (C.c_int, [vp]),
         "rxg_group_counters_read": (C.c_int, [vp, vp]),
+        "rxg_group_counters_rccl": (C.c_int, [vp]),
         "rxg_group_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -730,6 +731,12 @@ class Group:
         out = np.zeros(NCOUNTERS, dtype=np.uint64)
         _gcheck(_lib.rxg_group_counters_read(self.g, _ptr(out)), "rxg_group_counters_read")
         return out
+
+    def counters_rccl(self) -> bool:
+        """True when the counter merge is an RCCL all-reduce (members on distinct GPUs)."""
+        rc = _lib.rxg_group_counters_rccl(self.g)
+        _gcheck(min(rc, 0), "rxg_group_counters_rccl")
+        return rc == 1
 
 
 def synthetic_tcb_table(nflows: int, dst_raw: int = None, dport: int = 80):

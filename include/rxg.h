@@ -573,8 +573,12 @@ int rxg_group_payload_take(rxg_group *g, int32_t idx, uint32_t seq, uint32_t len
 /* Index of the member being replayed, -1 outside rxg_group_rx_replay. */
 int32_t rxg_group_replaying(rxg_group *g);
 int rxg_group_counters_reset(rxg_group *g);
-/* The members' counters summed. */
+/* The members' counters summed: an RCCL all-reduce (sum, uint64) of the members' counter
+   blocks over xGMI when the members are distinct GPUs (one communicator per member,
+   ncclCommInitAll at the first call), else summed on the host (members sharing a GPU). */
 int rxg_group_counters_read(rxg_group *g, uint64_t *out);
+/* 1 when rxg_group_counters_read merges with RCCL, 0 when on the host; negative on error. */
+int rxg_group_counters_rccl(rxg_group *g);
 /* Last error of a group call on this thread (member errors carry their text). */
 const char *rxg_group_last_error(void);
 

@@ -166,3 +166,26 @@ def test_group_posted_writes_and_errors():
         ptrs = (C.c_void_p * len(big))()
         with pytest.raises(rxg.RxgError, match="last group burst failed"):
             g.rx_replay(ops, ptrs, ptrs, recs.ctypes.data, len(big), 16)
+
+
+def test_group_counter_merge_rccl():
+    """rxg_group_counters_read merges with an RCCL all-reduce when the members are distinct
+    GPUs (one rank each; every GPU of the box, one on the test box) and on the host when
+    they share one; both equal the oracle's counters of the burst, and a second merge does
+    not double-count (the all-reduce writes a separate block)."""
+    import oracle
+    import torch
+    rows, frames = scenario(9, n=1500, closed=0.05)
+    tcb, live = pktgen.table_arrays(rows)
+    arena, off, lens = pktgen.pack_arena(frames)
+    _, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+    for devs, rccl in ((list(range(torch.cuda.device_count())), True), ([0, 0], False)):
+        with rxg.Group(devs, **MB) as g:
+            assert g.counters_rccl() == rccl
+            g.tcb_load(tcb, live)
+            g.counters_reset()
+            g.rx_burst(frames, rxg.REC16)
+            assert g.counters().tolist() == ecnt.tolist()
+            assert g.counters().tolist() == ecnt.tolist()
+            g.rx_burst(frames, rxg.REC16)
+            assert g.counters().tolist() == (2 * ecnt).tolist()
