@@ -160,8 +160,9 @@ def test_multi_burst_replay_sequential_equivalence(replay_engine, seed):
             ptrs = (C.c_void_p * cuts[1])(*[C.addressof(x) for x in bufs[:cuts[1]]])
             engine.rx_bursts_dev(d_arena.ptr, bursts, rxg.REC16)
             engine.sync()
-            assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs0.ctypes.data, cuts[1], 16) == 0
-            assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs0.ctypes.data, cuts[1], 16) == -22
+            none = rxg.HandoffOps()  # no handlers: only the cursor is under test here
+            assert lib.rxg_rx_replay(engine.ctx, C.byref(none), ptrs, ptrs, recs0.ctypes.data, cuts[1], 16) == 0
+            assert lib.rxg_rx_replay(engine.ctx, C.byref(none), ptrs, ptrs, recs0.ctypes.data, cuts[1], 16) == -22
     finally:
         for d in dev + [d_arena]:
             d.free()
