@@ -694,6 +694,7 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
     L.nbursts = 1;
     L.mode = 0;
     L.counters = nullptr;
+    L.variant = c->variant;
     L.max_blocks = c->max_blocks ? c->max_blocks : c->grid_tx;
     if (L.max_blocks == 0) L.max_blocks = 1024;
     HIP_OK(launch_rx(L, pick(c, stream)));
