@@ -155,7 +155,7 @@ def time_workload(eng, wl, steps, warmup, device, stream):
     return elapsed, kern_ms
 
 
-def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20):
+def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=rxg.REC16):
     """C2 (configs[1]: 2^20 x 64 B, 1 flow) as a ring of `nbursts` distinct 2^20-frame bursts
     in one 1 GiB frame pool (the same working set as the rotating C2 leg, beyond the 256 MB
     Infinity Cache), classified by ONE launch (rxg_rx_bursts_dev) instead of one launch per
@@ -164,12 +164,12 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20):
     pool = eng.synth(n=n * nbursts, nflows=1, len_a=64, mix=0, seed=seed + 123)
     tcb, live = rxg.synthetic_tcb_table(1)
     eng.tcb_load(tcb, live)
-    out = eng.alloc(n * nbursts * 16)
-    bursts = [(pool["off64"].ptr + j * n * 4, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * 16)
+    out = eng.alloc(n * nbursts * rec)
+    bursts = [(pool["off64"].ptr + j * n * 4, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * rec)
               for j in range(nbursts)]
     try:
         for _ in range(warmup):
-            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rxg.REC16)
+            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
         eng.sync()
         eng.counters_reset()
         evs = [(eng.event(), eng.event()) for _ in range(steps)]
@@ -177,7 +177,7 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20):
         t0 = time.perf_counter()
         for a, b in evs:
             eng.record(a)
-            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rxg.REC16)
+            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
             eng.record(b)
         eng.sync()
         barrier(device)
@@ -186,16 +186,18 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20):
         c = merge_counters(eng.counters(), device)
         frames_all = int(sum_over_ranks(n * nbursts, device)) * steps
         alg = n * nbursts * 64
-        rec = out.download(rxg.REC16_DTYPE, 4096, offset_bytes=(n * nbursts - 4096) * 16)
-        return {"bursts_per_launch": nbursts, "frames_per_burst": n,
-                "traffic_bytes_per_launch": traffic_of("c2_64B_1flow_multiburst", n, 16)[0],
+        last = out.download(rxg.rec_dtype(rec), 4096, offset_bytes=(n * nbursts - 4096) * rec)
+        if rec == rxg.REC8:
+            last = rxg.rec8_expand(last)
+        return {"bursts_per_launch": nbursts, "frames_per_burst": n, "rec_kind": rec,
+                "traffic_bytes_per_launch": traffic_of("c2_64B_1flow_multiburst", n, rec)[0],
                 "algorithmic_bytes_per_launch": alg,
                 "kernel_us_per_launch": round(k * 1e6, 2), "kernel_us_per_burst": round(k * 1e6 / nbursts, 2),
                 "mpps": round(frames_all / dt / 1e6, 2), "gbs": round(frames_all * 64 / dt / 1e9, 2),
                 "roofline_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4), "working_set_GiB": round(alg / 2**30, 3),
                 "counters_ok": bool(int(c[0]) == frames_all and int(c[7]) == 0 and int(c[8]) == 0
                                     and int(c[13]) == frames_all
-                                    and (rec["verdict"] == rxg.V_DISPATCH).all() and (rec["tcb_idx"] == 1).all())}
+                                    and (last["verdict"] == rxg.V_DISPATCH).all() and (last["tcb_idx"] == 1).all())}
     finally:
         out.free()
         for v in pool.values():
@@ -479,7 +481,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3_1500B_1Kflows", choices=sorted(WORKLOADS))
     ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU per step")
-    ap.add_argument("--rec", type=int, default=16, choices=[16, 48])
+    ap.add_argument("--rec", type=int, default=16, choices=[8, 16, 48])
     ap.add_argument("--no-legs", action="store_true", help="skip the 64 B / IMIX legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -560,6 +562,9 @@ def main():
             }
             lw.free()
         legs["c2_64B_1flow_multiburst"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed)
+        # the same ring with 8-byte records (RXG_REC8): 8 of the 72 bytes per frame less
+        legs["c2_64B_1flow_multiburst_rec8"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed,
+                                                              rec=rxg.REC8)
         legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
         legs["tx_generate_dev"] = tx_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)

@@ -220,7 +220,7 @@ extern "C" int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32
                                   void *out_host)
 {
     if (!g || (n && (!pkts || !out_host))) return gfail(-EINVAL, "rxg_group_rx_burst: NULL argument");
-    if (rec_kind != RXG_REC16 && rec_kind != RXG_REC48)
+    if (rec_kind != RXG_REC8 && rec_kind != RXG_REC16 && rec_kind != RXG_REC48)
         return gfail(-EINVAL, "rxg_group_rx_burst: rec_kind %u", rec_kind);
     {  // the posted writes, on every member, before any shard reads its mirror
         const int rc = rxg_group_tcb_drain(g);

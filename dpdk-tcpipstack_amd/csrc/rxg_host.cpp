@@ -61,7 +61,7 @@ struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t max_blocks = 0;        // rxg_config.max_blocks: grid cap (0 = occupancy grid)
-    uint32_t grid_rec16 = 0, grid_rec48 = 0, grid_tx = 0;
+    uint32_t grid_rec8 = 0, grid_rec16 = 0, grid_rec48 = 0, grid_tx = 0;
     // Experiment switches: only an experiment build (make experiments, -DRXG_EXPERIMENTS,
     // rxg/librxg_exp.so for scripts/kbench.py and pgbench.py) reads them from the
     // environment; in the product library they stay 0.
@@ -224,6 +224,7 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) {
         // one generation of resident workgroups per CU (grid-stride over slices)
         const uint32_t cus = (uint32_t)prop.multiProcessorCount;
+        c->grid_rec8 = cus * (uint32_t)rx_blocks_per_cu(8);
         c->grid_rec16 = cus * (uint32_t)rx_blocks_per_cu(16);
         c->grid_rec48 = cus * (uint32_t)rx_blocks_per_cu(48);
         c->grid_tx = cus * (uint32_t)rx_blocks_per_cu(0);
@@ -606,10 +607,12 @@ static void select_burst(rxg_ctx *c, uint32_t j)
 
 // Classify bursts[0..k) of one frame pool against the mirror as it stands: one launch per
 // kMaxBursts bursts.  The bursts are then replayed in order (rxg_rx_replay).
+static bool rec_kind_ok(uint32_t k) { return k == RXG_REC8 || k == RXG_REC16 || k == RXG_REC48; }
+
 static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
                          void *stream, const char *who)
 {
-    if (rec_kind != RXG_REC16 && rec_kind != RXG_REC48) return fail(-EINVAL, "%s: rec_kind %u", who, rec_kind);
+    if (!rec_kind_ok(rec_kind)) return fail(-EINVAL, "%s: rec_kind %u", who, rec_kind);
     if (k && !bursts) return fail(-EINVAL, "%s: NULL burst table", who);
     bool any = false;
     for (uint32_t j = 0; j < k; ++j) {
@@ -653,7 +656,8 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
         L.mode = (int)rec_kind;
         L.table = table_view(c);
         L.counters = c->nocount ? nullptr : c->counters;
-        L.max_blocks = c->max_blocks ? c->max_blocks : (rec_kind == RXG_REC48 ? c->grid_rec48 : c->grid_rec16);
+        L.max_blocks = c->max_blocks ? c->max_blocks : (rec_kind == RXG_REC48 ? c->grid_rec48
+                                                        : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
         if (L.max_blocks == 0) L.max_blocks = 1024;
         L.variant = c->variant;
         HIP_OK(launch_rx(L, st));
@@ -705,8 +709,7 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
                             void *out_host)
 {
     if (!c || (n && (!pkts || !out_host))) return fail(-EINVAL, "rxg_rx_burst: NULL argument");
-    if (rec_kind != RXG_REC16 && rec_kind != RXG_REC48)
-        return fail(-EINVAL, "rxg_rx_burst: rec_kind %u", rec_kind);
+    if (!rec_kind_ok(rec_kind)) return fail(-EINVAL, "rxg_rx_burst: rec_kind %u", rec_kind);
     if (n > c->max_batch)
         return fail(-EINVAL, "rxg_rx_burst: n=%u exceeds max_batch=%u", n, c->max_batch);
     c->burst_ok = false;
@@ -1028,7 +1031,7 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
 {
     if (!c || !ops || (n && (!mbufs || !frames || !recs)))
         return fail(-EINVAL, "rxg_rx_replay: NULL argument");
-    if (stride != RXG_REC16 && stride != RXG_REC48) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
+    if (!rec_kind_ok(stride)) return fail(-EINVAL, "rxg_rx_replay: stride %u", stride);
     if (n && c->last_n != n)
         return fail(-EINVAL, "rxg_rx_replay: n=%u but the burst to replay (%u of the last launch) had %u frames", n,
                     c->replay_cursor, c->last_n);
@@ -1042,7 +1045,10 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
     } pos_guard{c};
     std::vector<rxg_rec16> &cur = c->rp_cur;
     cur.resize(n);
-    for (uint32_t i = 0; i < n; ++i) cur[i] = *(const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
+    if (stride == RXG_REC8)
+        for (uint32_t i = 0; i < n; ++i) rxg_rec8_expand((const rxg_rec8 *)recs + i, &cur[i]);
+    else
+        for (uint32_t i = 0; i < n; ++i) cur[i] = *(const rxg_rec16 *)((const uint8_t *)recs + (size_t)i * stride);
     int64_t delta[RXG_NCOUNTERS] = {0};
 
     // Staleness by write sequence numbers, checked when a packet is reached (its header is

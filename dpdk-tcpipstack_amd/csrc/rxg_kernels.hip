@@ -918,7 +918,11 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
     const int32_t datalen = (int32_t)tl - (int32_t)(vihl & 0xFu) * 4 - (int32_t)(doff >> 4) * 4;
 
     (void)f;
-    {
+    if constexpr (MODE == 8) {  // rxg_rec8 (rxg.h)
+        const uint32_t st3 = st == RXG_STATE_NONE ? 7u : st;
+        pr.q0.x = ((uint32_t)(idx + 1) & 0xFFFFFFu) | (verdict << 24) | (st3 << 27);
+        pr.q0.y = tflags | (flags << 8) | (((uint32_t)(datalen + 128) & 0x1FFFFu) << 14);
+    } else {
         uint4 q0;
         q0.x = (uint32_t)idx;
         q0.y = ipc | (tcc << 16);
@@ -1036,10 +1040,15 @@ __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane,
 // at the end): record stores interleaved with the frame stream cost ≈10 % of the C3 kernel
 // (measured: 271 µs with 1 KiB stored per slice as it completes, 244 µs staged and
 // written at the end, 243 µs with no record stores at all), HBM read/write turnarounds.
+// Record bytes of one slice (64 frames) in the ring, in uint4: REC8 512 B, REC16 1 KiB,
+// REC48 3 KiB.
+constexpr int ring_slot_u4(int mode) { return mode * 64 / 16; }
+
 template <int MODE, int RS>
 struct RecRing {
-    static constexpr int kQ = MODE / 16;  // uint4 per record
-    uint4 (*img)[kQ * 64];                // [RS][kQ * 64]: the slice's records, contiguous
+    static constexpr int kQ = MODE / 16;  // uint4 per record (REC16 / REC48)
+    static constexpr int kSlot = ring_slot_u4(MODE);
+    uint4 (*img)[kSlot];                  // [RS][kSlot]: the slice's records, contiguous
     uint32_t *base;                       // [RS]: the slot's launch slice
     uint32_t n = 0;                       // slots in use (wave-uniform)
 
@@ -1050,18 +1059,22 @@ struct RecRing {
     template <bool NTS = false, typename BC>
     __device__ __forceinline__ uint32_t *scratch(const RxArgs &a, int lane, int bytes, BC &bc)
     {
-        const uint32_t need = (uint32_t)((bytes + kQ * 1024 - 1) / (kQ * 1024));
+        const uint32_t need = (uint32_t)((bytes + kSlot * 16 - 1) / (kSlot * 16));
         if (n + need > (uint32_t)RS) flush<NTS>(a, lane, bc);
         return reinterpret_cast<uint32_t *>(img[n]);
     }
 
     __device__ __forceinline__ void put(uint32_t slice, int lane, const Rec &r)
     {
-        uint4 *q = img[n] + lane * kQ;
-        q[0] = r.q0;
-        if constexpr (kQ == 3) {
-            q[1] = r.q1;
-            q[2] = r.q2;
+        if constexpr (MODE == 8) {
+            reinterpret_cast<uint2 *>(img[n])[lane] = make_uint2(r.q0.x, r.q0.y);
+        } else {
+            uint4 *q = img[n] + lane * kQ;
+            q[0] = r.q0;
+            if constexpr (kQ == 3) {
+                q[1] = r.q1;
+                q[2] = r.q2;
+            }
         }
         if (lane == 0) base[n] = slice;
         ++n;
@@ -1082,6 +1095,21 @@ struct RecRing {
             const uint32_t kb = bc.of(a, sl);
             const uint32_t f0 = (sl - bc.slice0_of(a, kb)) * 64u;  // first frame of the slice in its burst
             const uint32_t nb = bc.n_of(a, kb);
+            if constexpr (MODE == 8) {  // 64 lanes x 8 B: 512 B contiguous per instruction
+                uint2 *d8 = reinterpret_cast<uint2 *>(bc.out_of(a, kb) + (size_t)f0 * 8u);
+                if (f0 + (uint32_t)lane < nb) {
+                    const uint2 q = reinterpret_cast<const uint2 *>(img[i])[lane];
+                    if constexpr (NTS) {
+                        typedef unsigned int v2 __attribute__((ext_vector_type(2)));
+                        v2 v;
+                        v.x = q.x; v.y = q.y;
+                        __builtin_nontemporal_store(v, reinterpret_cast<v2 *>(d8 + lane));
+                    } else {
+                        d8[lane] = q;
+                    }
+                }
+                continue;
+            }
             uint4 *dst = reinterpret_cast<uint4 *>(bc.out_of(a, kb) + (size_t)f0 * MODE);
 #pragma unroll
             for (int k = 0; k < kQ; ++k) {
@@ -1151,10 +1179,11 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     // 3 workgroups per CU: the best of 2-5 per CU over C2, C3, C4); its
     // free slots are also the scratch of the slice in progress (4 KiB small-slice transpose,
     // NF x 256 B parked fields), so LDS per wave is the ring alone and sets the occupancy.
-    constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : 1;
-    constexpr int kQ = MODE == 0 ? 1 : MODE / 16;
-    static_assert(MODE == 0 || RS * kQ * 1024 >= 4096 + kQ * 1024, "ring too small for the scratch");
-    __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kQ * 64];
+    // REC8: 22 slots of 512 B (the same 11 KiB per wave as REC16's ring)
+    constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : MODE == 8 ? 2 * RS16 : 1;
+    constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE);
+    static_assert(MODE == 0 || RS * kSlot * 16 >= 4096 + kSlot * 16, "ring too small for the scratch");
+    __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kSlot];
     __shared__ uint32_t s_recf[4][RS];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
@@ -1434,6 +1463,11 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         else
             hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
 #endif
+    } else if (L.mode == 8) {
+        if (a.nbursts > 1)
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (L.mode == 48) {
         if (a.nbursts > 1)
             hipLaunchKernelGGL((rx_kernel<48, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
@@ -1479,7 +1513,9 @@ int rx_blocks_per_cu(int mode)
 {
     int n = 0;
     hipError_t e;
-    if (mode == 16)
+    if (mode == 8)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<8, 0xFF, true>, 256, 0);
+    else if (mode == 16)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<16, 0xFF, true>, 256, 0);
     else if (mode == 48)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<48, 0xFF, true>, 256, 0);

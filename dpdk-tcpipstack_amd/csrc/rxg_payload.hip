@@ -77,12 +77,27 @@ __device__ __forceinline__ Cand candidate(const PgArgs &a, uint32_t i)
     // the record, the descriptor and the length are loaded together (one HBM round trip
     // before the frame's header word, not two)
     // rxg_rec16: x tcb_idx | y checksums | z verdict, state<<8, tcp_flags<<16, flags<<24 | w datalen
-    const uint4 r = *reinterpret_cast<const uint4 *>(a.recs + (size_t)i * a.stride);
-    const uint32_t off = a.off64[i];
-    const uint32_t flen = a.len[i];
-    asm volatile("" ::"v"(off), "v"(flen));  // keeps the two loads above the branch
-    const uint32_t verdict = r.z & 0xFFu, rflags = r.z >> 24;
-    const int32_t datalen = (int32_t)r.w;
+    // rxg_rec8 (stride 8): w0 verdict at 24 | w1 flags at 8, datalen + 128 at 14
+    uint32_t verdict, rflags;
+    int32_t datalen;
+    uint32_t off, flen;
+    if (a.stride == 8u) {
+        const uint2 r = *reinterpret_cast<const uint2 *>(a.recs + (size_t)i * 8u);
+        off = a.off64[i];
+        flen = a.len[i];
+        asm volatile("" ::"v"(off), "v"(flen));
+        verdict = (r.x >> 24) & 7u;
+        rflags = (r.y >> 8) & 0x3Fu;
+        datalen = (int32_t)((r.y >> 14) & 0x1FFFFu) - 128;
+    } else {
+        const uint4 r = *reinterpret_cast<const uint4 *>(a.recs + (size_t)i * a.stride);
+        off = a.off64[i];
+        flen = a.len[i];
+        asm volatile("" ::"v"(off), "v"(flen));  // keeps the two loads above the branch
+        verdict = r.z & 0xFFu;
+        rflags = r.z >> 24;
+        datalen = (int32_t)r.w;
+    }
     if (verdict > RXG_V_RST_LISTEN_NONSYN || datalen <= 0 || (rflags & RXG_F_TRUNC)) return c;
     const uint64_t base = (uint64_t)off * 64u;
     // bytes 44..47 of the frame (>= 54 bytes: not RXG_F_TRUNC); data_off is byte 46

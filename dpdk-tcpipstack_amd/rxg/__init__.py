@@ -31,7 +31,7 @@ STATE_NONE = 0xFF
 
 V_DISPATCH, V_RST_NOPCB, V_RST_LISTEN_NONSYN, V_DROP_NONTCP, V_ARP, V_DROP_L2 = range(6)
 F_IP_OK, F_TCP_OK, F_LISTEN, F_REF_NULLSLOT, F_TRUNC, F_ARP_LEARN = 1, 2, 4, 8, 16, 32
-REC16, REC48 = 16, 48
+REC8, REC16, REC48 = 8, 16, 48
 
 COUNTERS = ["rx", "bytes", "ipv4", "arp", "other_l2", "tcp", "non_tcp", "ip_cksum_bad",
             "tcp_cksum_bad", "tcb_hit_exact", "tcb_hit_listen", "nopcb", "listen_nonsyn",
@@ -53,6 +53,42 @@ TCB_DTYPE = np.dtype([("dport", "<i4"), ("sport", "<i4"), ("ipv4_dst", "<u4"),
                       ("ipv4_src", "<u4"), ("state", "u1"), ("pad", "u1"),
                       ("identifier", "<u2")])
 assert REC16_DTYPE.itemsize == 16 and REC48_DTYPE.itemsize == 48 and TCB_DTYPE.itemsize == 20
+REC8_DTYPE = np.dtype([("w0", "<u4"), ("w1", "<u4")])
+
+
+def rec8_pack(r16: np.ndarray) -> np.ndarray:
+    """rxg_rec16 -> rxg_rec8 (rxg.h): the record the kernel writes for RXG_REC8."""
+    out = np.zeros(len(r16), dtype=REC8_DTYPE)
+    st = r16["state"].astype(np.uint32)
+    st[st == STATE_NONE] = 7
+    out["w0"] = (((r16["tcb_idx"].astype(np.int64) + 1) & 0xFFFFFF).astype(np.uint32)
+                 | (r16["verdict"].astype(np.uint32) << 24) | (st << 27))
+    out["w1"] = (r16["tcp_flags"].astype(np.uint32) | (r16["flags"].astype(np.uint32) << 8)
+                 | (((r16["datalen"].astype(np.int64) + 128) & 0x1FFFF).astype(np.uint32) << 14))
+    return out
+
+
+def rec8_expand(r8: np.ndarray) -> np.ndarray:
+    """rxg_rec8 -> rxg_rec16 as rxg_rec8_expand (rxg.h) does it: a checksum the record
+    knows only as 'not zero' reads 0xFFFF."""
+    w0, w1 = r8["w0"].astype(np.uint32), r8["w1"].astype(np.uint32)
+    out = np.zeros(len(r8), dtype=REC16_DTYPE)
+    v = (w0 >> 24) & 7
+    st = (w0 >> 27) & 7
+    fl = (w1 >> 8) & 0x3F
+    out["tcb_idx"] = (w0 & 0xFFFFFF).astype(np.int32) - 1
+    out["ip_cksum"] = np.where((v <= V_DROP_NONTCP) & ((fl & F_IP_OK) == 0), 0xFFFF, 0)
+    out["tcp_cksum"] = np.where((v <= V_RST_LISTEN_NONSYN) & ((fl & F_TCP_OK) == 0), 0xFFFF, 0)
+    out["verdict"] = v
+    out["state"] = np.where(st == 7, STATE_NONE, st)
+    out["tcp_flags"] = w1 & 0xFF
+    out["flags"] = fl
+    out["datalen"] = ((w1 >> 14) & 0x1FFFF).astype(np.int32) - 128
+    return out
+
+
+def rec_dtype(rec_kind: int) -> np.dtype:
+    return {REC8: REC8_DTYPE, REC16: REC16_DTYPE, REC48: REC48_DTYPE}[rec_kind]
 
 
 class RxgError(RuntimeError):
@@ -500,7 +536,7 @@ class Engine:
                  rec_kind: int = REC48) -> np.ndarray:
         """Upload a packed arena, run one burst, return the records (numpy)."""
         n = len(lens)
-        dt = REC48_DTYPE if rec_kind == REC48 else REC16_DTYPE
+        dt = rec_dtype(rec_kind)
         if n == 0:
             return np.zeros(0, dtype=dt)
         da, do, dl = self.to_device(arena), self.to_device(off64), self.to_device(lens)
@@ -534,7 +570,7 @@ class Engine:
         views = (PktView * max(n, 1))()
         for i, b in enumerate(bufs):
             views[i] = PktView(C.addressof(b), 0, len(frames[i]), 0)
-        dt = REC48_DTYPE if rec_kind == REC48 else REC16_DTYPE
+        dt = rec_dtype(rec_kind)
         out = np.zeros(n, dtype=dt)
         _check(_lib.rxg_rx_burst(self.ctx, views, n, rec_kind, _ptr(out) if n else None),
                "rxg_rx_burst")
@@ -704,7 +740,7 @@ class Group:
         views = (PktView * max(n, 1))()
         for i, b in enumerate(bufs):
             views[i] = PktView(C.addressof(b), 0, len(frames[i]), 0)
-        dt = REC48_DTYPE if rec_kind == REC48 else REC16_DTYPE
+        dt = rec_dtype(rec_kind)
         out = np.zeros(n, dtype=dt)
         _gcheck(_lib.rxg_group_rx_burst(self.g, views, n, rec_kind, _ptr(out) if n else None),
                 "rxg_group_rx_burst")

@@ -136,7 +136,36 @@ typedef struct rxg_rec48 {
 } rxg_rec48;
 /* total_length = c.datalen + (version_ihl & 0xf) * 4 + (data_off >> 4) * 4. */
 
-enum rxg_rec_kind { RXG_REC16 = 16, RXG_REC48 = 48 };
+/* 8-byte record (RXG_REC8): what rxg_rx_replay and rxg_payload_gather_dev use, half the
+   bytes of rxg_rec16 per frame; the two checksums are carried as RXG_F_IP_OK /
+   RXG_F_TCP_OK only.
+     w0  bits  0-23  tcb_idx + 1 (0: findtcb returned NULL)
+         bits 24-26  verdict (enum rxg_verdict)
+         bits 27-29  state (7: RXG_STATE_NONE)
+     w1  bits  0-7   tcp_flags
+         bits  8-13  flags (enum rxg_rec_flag)
+         bits 14-30  datalen + 128 (datalen >= -120: total_length - 60 - 60)           */
+typedef struct rxg_rec8 {
+    uint32_t w0, w1;
+} rxg_rec8;
+
+enum rxg_rec_kind { RXG_REC8 = 8, RXG_REC16 = 16, RXG_REC48 = 48 };
+
+/* rxg_rec8 -> rxg_rec16.  A checksum the record only knows as "not 0x0000" reads 0xFFFF
+   (IPv4 frames without RXG_F_IP_OK, TCP segments without RXG_F_TCP_OK); the others 0. */
+static inline void rxg_rec8_expand(const rxg_rec8 *r, rxg_rec16 *o)
+{
+    const uint32_t v = (r->w0 >> 24) & 7u, st = (r->w0 >> 27) & 7u, fl = (r->w1 >> 8) & 0x3Fu;
+    const int ip = v <= RXG_V_DROP_NONTCP, tcp = v <= RXG_V_RST_LISTEN_NONSYN;
+    o->tcb_idx = (int32_t)(r->w0 & 0xFFFFFFu) - 1;
+    o->ip_cksum = (uint16_t)((ip && !(fl & RXG_F_IP_OK)) ? 0xFFFFu : 0u);
+    o->tcp_cksum = (uint16_t)((tcp && !(fl & RXG_F_TCP_OK)) ? 0xFFFFu : 0u);
+    o->verdict = (uint8_t)v;
+    o->state = (uint8_t)(st == 7u ? RXG_STATE_NONE : st);
+    o->tcp_flags = (uint8_t)(r->w1 & 0xFFu);
+    o->flags = (uint8_t)fl;
+    o->datalen = (int32_t)((r->w1 >> 14) & 0x1FFFFu) - 128;
+}
 
 /* ------------------------------------------------------------------------- */
 /* Per-GPU counters (merged across GPUs with an RCCL all-reduce, sum, uint64). */
@@ -275,7 +304,7 @@ typedef struct rxg_dev_batch {
     const uint32_t *off64;  /* dev, n entries, in 64-byte units */
     const uint16_t *len;    /* dev, n entries */
     uint32_t n;
-    uint32_t rec_kind;      /* RXG_REC16 or RXG_REC48 */
+    uint32_t rec_kind;      /* RXG_REC8, RXG_REC16 or RXG_REC48 */
     void *out;              /* dev, n records of rec_kind bytes */
 } rxg_dev_batch;
 

@@ -89,9 +89,11 @@ def _check(engine, rows, frames, rec_kind):
     exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
     if rec_kind == rxg.REC16:
         exp = exp["c"]
+    elif rec_kind == rxg.REC8:
+        exp = rxg.rec8_pack(exp["c"])
     if got.tobytes() != exp.tobytes():
-        g = got if rec_kind == rxg.REC16 else got["c"]
-        e = exp if rec_kind == rxg.REC16 else exp["c"]
+        g = got if rec_kind != rxg.REC48 else got["c"]
+        e = exp if rec_kind != rxg.REC48 else exp["c"]
         gb = g.view(np.uint8).reshape(len(frames), -1)
         eb = e.view(np.uint8).reshape(len(frames), -1)
         bad = np.nonzero((gb != eb).any(axis=1))[0]
@@ -102,7 +104,7 @@ def _check(engine, rows, frames, rec_kind):
 
 
 @pytest.mark.parametrize("seed", [21, 22])
-@pytest.mark.parametrize("rec_kind", [rxg.REC16, rxg.REC48])
+@pytest.mark.parametrize("rec_kind", [rxg.REC8, rxg.REC16, rxg.REC48])
 def test_many_slices_per_wave(small_grid_engine, seed, rec_kind):
     rows, frames = _batch(seed)
     _check(small_grid_engine, rows, frames, rec_kind)
@@ -114,3 +116,4 @@ def test_partial_last_slice_after_small_run(small_grid_engine):
     rows, frames = _batch(23)
     frames = frames[:64 * 30 + 37]
     _check(small_grid_engine, rows, frames, rxg.REC48)
+    _check(small_grid_engine, rows, frames, rxg.REC8)

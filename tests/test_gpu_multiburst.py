@@ -9,6 +9,8 @@
   burst sees the writes its predecessors' replays made (tcp_listen children, remove_tcb,
   state changes; tcp_states.c:150-219).
 * A payload gather between replays covers the burst to be replayed next.
+* The same with 8-byte records (RXG_REC8): the kernel's packing equals the oracle's record
+  packed (rxg.rec8_pack), and replay and gather read them.
 """
 import ctypes as C
 import random
@@ -44,8 +46,8 @@ def _cuts(rng, n, k):
     return [0] + c + [n]
 
 
-@pytest.mark.parametrize("k,seed", [(5, 1), (40, 2)])
-def test_multi_burst_records_equal_single_bursts_and_oracle(engine, k, seed):
+@pytest.mark.parametrize("k,seed,kind", [(5, 1, rxg.REC48), (40, 2, rxg.REC48), (5, 3, rxg.REC8), (40, 4, rxg.REC8)])
+def test_multi_burst_records_equal_single_bursts_and_oracle(engine, k, seed, kind):
     rng = random.Random(seed)
     rows, frames = pktgen.parity_set(seed=100 + seed, n=6000)
     # a run of small frames so all-small slices appear inside some bursts
@@ -69,20 +71,22 @@ def test_multi_burst_records_equal_single_bursts_and_oracle(engine, k, seed):
             a, b = cuts[j], cuts[j + 1]
             do = engine.to_device(off[a:b] if b > a else np.zeros(1, np.uint32))
             dl = engine.to_device(lens[a:b] if b > a else np.zeros(1, np.uint16))
-            dout = engine.alloc(max(b - a, 1) * 48)
+            dout = engine.alloc(max(b - a, 1) * kind)
             dev += [do, dl, dout]
             bursts.append((do.ptr, dl.ptr, b - a, dout.ptr))
         engine.counters_reset()
-        engine.rx_bursts_dev(d_arena.ptr, bursts, rxg.REC48)
+        engine.rx_bursts_dev(d_arena.ptr, bursts, kind)
         engine.sync()
         cnt = engine.counters()
-        got = np.concatenate([dev[3 * j + 2].download(rxg.REC48_DTYPE, cuts[j + 1] - cuts[j]) for j in range(k)])
+        got = np.concatenate([dev[3 * j + 2].download(rxg.rec_dtype(kind), cuts[j + 1] - cuts[j]) for j in range(k)])
         parr, poff, plens = pktgen.pack_arena(frames)
         exp, ecnt = oracle.rx_batch(parr, poff, plens, tcb, live)
+        if kind == rxg.REC8:
+            exp = rxg.rec8_pack(exp["c"])
         assert got.tobytes() == exp.tobytes()
         assert cnt.tolist() == ecnt.tolist()
         # one burst at a time through the single-burst entry point: the same records
-        single = np.concatenate([engine.rx_arena(*pktgen.pack_arena(frames[cuts[j]:cuts[j + 1]]), rxg.REC48)
+        single = np.concatenate([engine.rx_arena(*pktgen.pack_arena(frames[cuts[j]:cuts[j + 1]]), kind)
                                  for j in range(k)])
         assert single.tobytes() == got.tobytes()
     finally:
@@ -90,8 +94,8 @@ def test_multi_burst_records_equal_single_bursts_and_oracle(engine, k, seed):
             d.free()
 
 
-@pytest.mark.parametrize("seed", [4, 5])
-def test_multi_burst_replay_sequential_equivalence(replay_engine, seed):
+@pytest.mark.parametrize("seed,kind", [(4, rxg.REC16), (5, rxg.REC16), (6, rxg.REC8)])
+def test_multi_burst_replay_sequential_equivalence(replay_engine, seed, kind):
     engine = replay_engine
     rows, frames = scenario(seed, n=1500, closed=0.05)
     exp, ecnt, erows = sequential_reference(rows, frames)
@@ -109,7 +113,7 @@ def test_multi_burst_replay_sequential_equivalence(replay_engine, seed):
     dev, bursts = [], []
     for j in range(k):
         a, b = cuts[j], cuts[j + 1]
-        do, dl, dout = engine.to_device(off[a:b]), engine.to_device(lens[a:b]), engine.alloc((b - a) * 16)
+        do, dl, dout = engine.to_device(off[a:b]), engine.to_device(lens[a:b]), engine.alloc((b - a) * kind)
         dev += [do, dl, dout]
         bursts.append((do.ptr, dl.ptr, b - a, dout.ptr))
     model = Model(rows, engine)
@@ -137,13 +141,13 @@ def test_multi_burst_replay_sequential_equivalence(replay_engine, seed):
     lib = rxg.load_library()
     try:
         engine.counters_reset()
-        engine.rx_bursts_dev(d_arena.ptr, bursts, rxg.REC16)
+        engine.rx_bursts_dev(d_arena.ptr, bursts, kind)
         engine.sync()
         for j in range(k):
             a, b = cuts[j], cuts[j + 1]
-            recs = dev[3 * j + 2].download(rxg.REC16_DTYPE, b - a)
+            recs = dev[3 * j + 2].download(rxg.rec_dtype(kind), b - a)
             ptrs = (C.c_void_p * (b - a))(*[C.addressof(x) for x in bufs[a:b]])
-            rc = lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, b - a, 16)
+            rc = lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, b - a, kind)
             assert rc == 0, lib.rxg_last_error()
         for i, (v, idx, st) in enumerate(exp):
             if v == rxg.V_DISPATCH:
@@ -156,19 +160,20 @@ def test_multi_burst_replay_sequential_equivalence(replay_engine, seed):
         assert engine.counters().tolist() == ecnt.tolist()
         # replaying out of order is refused (the next burst has another size)
         if cuts[2] - cuts[1] != cuts[1] - cuts[0]:
-            recs0 = dev[2].download(rxg.REC16_DTYPE, cuts[1])
+            recs0 = dev[2].download(rxg.rec_dtype(kind), cuts[1])
             ptrs = (C.c_void_p * cuts[1])(*[C.addressof(x) for x in bufs[:cuts[1]]])
-            engine.rx_bursts_dev(d_arena.ptr, bursts, rxg.REC16)
+            engine.rx_bursts_dev(d_arena.ptr, bursts, kind)
             engine.sync()
             none = rxg.HandoffOps()  # no handlers: only the cursor is under test here
-            assert lib.rxg_rx_replay(engine.ctx, C.byref(none), ptrs, ptrs, recs0.ctypes.data, cuts[1], 16) == 0
-            assert lib.rxg_rx_replay(engine.ctx, C.byref(none), ptrs, ptrs, recs0.ctypes.data, cuts[1], 16) == -22
+            assert lib.rxg_rx_replay(engine.ctx, C.byref(none), ptrs, ptrs, recs0.ctypes.data, cuts[1], kind) == 0
+            assert lib.rxg_rx_replay(engine.ctx, C.byref(none), ptrs, ptrs, recs0.ctypes.data, cuts[1], kind) == -22
     finally:
         for d in dev + [d_arena]:
             d.free()
 
 
-def test_multi_burst_gather_follows_the_replay_cursor(engine):
+@pytest.mark.parametrize("kind", [rxg.REC16, rxg.REC8])
+def test_multi_burst_gather_follows_the_replay_cursor(engine, kind):
     """rxg_payload_gather_dev after a multi-burst launch gathers the burst to be replayed
     next; after that burst's replay, the next one."""
     rng = random.Random(8)
@@ -182,7 +187,7 @@ def test_multi_burst_gather_follows_the_replay_cursor(engine):
     dev, bursts = [], []
     for j in range(3):
         a, b = cuts[j], cuts[j + 1]
-        do, dl, dout = engine.to_device(off[a:b]), engine.to_device(lens[a:b]), engine.alloc((b - a) * 16)
+        do, dl, dout = engine.to_device(off[a:b]), engine.to_device(lens[a:b]), engine.alloc((b - a) * kind)
         dev += [do, dl, dout]
         bursts.append((do.ptr, dl.ptr, b - a, dout.ptr))
     from oracle import payload as opl
@@ -190,17 +195,18 @@ def test_multi_burst_gather_follows_the_replay_cursor(engine):
     ops = rxg.HandoffOps()
     bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
     try:
-        engine.rx_bursts_dev(d_arena.ptr, bursts, rxg.REC16)
+        engine.rx_bursts_dev(d_arena.ptr, bursts, kind)
         engine.sync()
         for j in range(3):
             a, b = cuts[j], cuts[j + 1]
-            recs = dev[3 * j + 2].download(rxg.REC16_DTYPE, b - a)
-            e_msgs, e_arena, e_used = opl.gather(frames[a:b], recs, 1 << 40)
+            recs = dev[3 * j + 2].download(rxg.rec_dtype(kind), b - a)
+            r16 = rxg.rec8_expand(recs) if kind == rxg.REC8 else recs
+            e_msgs, e_arena, e_used = opl.gather(frames[a:b], r16, 1 << 40)
             g_arena, g_msgs, g_used = engine.payload_gather(b - a, e_used)
             assert g_used == e_used and g_msgs.tobytes() == e_msgs.tobytes()
             assert g_arena[:len(e_arena)].tobytes() == e_arena.tobytes()
             ptrs = (C.c_void_p * (b - a))(*[C.addressof(x) for x in bufs[a:b]])
-            assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, b - a, 16) == 0
+            assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, b - a, kind) == 0
     finally:
         for d in dev + [d_arena]:
             d.free()
