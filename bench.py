@@ -37,7 +37,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.json",
                  ("c2_64B_1flow", 1 << 20, 16): "profiles/r02/c2/traffic.json",
                  ("c4_imix_64Kflows", 1 << 20, 16): "profiles/r02/c4/traffic.json",
-                 ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r02/c2multi/traffic.json"}
+                 ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r02/c2multi/traffic.json",
+                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r02/rec8/c3/traffic.json",
+                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r02/rec8/c2/traffic.json",
+                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r02/rec8/c4/traffic.json",
+                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r02/rec8/c2multi/traffic.json"}
 
 
 def traffic_of(name, n, rec):
@@ -328,8 +332,9 @@ def c5_leg(eng, n, steps, warmup, device, seed):
 
 def payload_leg(eng, wl, steps, warmup):
     """the device payload gather (rxg_payload_gather_dev) after a burst
-    of the workload.  Algorithmic bytes per launch = 2 x payload bytes (read + write) + 16 B
-    record read + 16 B descriptor write per frame; HIP events around the three launches."""
+    of the workload.  Algorithmic bytes per launch = 2 x payload bytes (read + write) + the
+    record read (wl.rec bytes) + 16 B descriptor write per frame; HIP events around the three
+    launches."""
     wl.launch(eng, 0)
     pl = (wl.lens.astype(np.int64) - 54).clip(min=0)  # synthetic frames: IHL 5, data_off 5
     dl = int(pl.sum())
@@ -346,9 +351,9 @@ def payload_leg(eng, wl, steps, warmup):
         eng.sync()
         ms = [eng.elapsed_ms(a, b) for a, b in evs]
         k = float(np.mean(ms)) / 1e3
-        alg = 2 * dl + 32 * wl.n
+        alg = 2 * dl + (wl.rec + 16) * wl.n
         assert int(used.download(np.uint64, 1)[0]) == cap
-        return {"payload_bytes": dl, "arena_bytes": cap,
+        return {"payload_bytes": dl, "arena_bytes": cap, "record_bytes": wl.rec,
                 "kernels_us": round(k * 1e6, 2), "achieved_GBps": round(alg / k / 1e9, 1),
                 "roofline_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": alg}
@@ -481,7 +486,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3_1500B_1Kflows", choices=sorted(WORKLOADS))
     ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU per step")
-    ap.add_argument("--rec", type=int, default=16, choices=[8, 16, 48])
+    # record kind: 8 = rxg_rec8, everything rxg_rx_replay and the payload gather read
+    # (checksums as ok bits); 16 / 48 carry the checksum values / every header field
+    ap.add_argument("--rec", type=int, default=8, choices=[8, 16, 48])
     ap.add_argument("--no-legs", action="store_true", help="skip the 64 B / IMIX legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -561,10 +568,19 @@ def main():
                 "algorithmic_bytes_per_launch": lw.bytes_per_batch,
             }
             lw.free()
-        legs["c2_64B_1flow_multiburst"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed)
-        # the same ring with 8-byte records (RXG_REC8): 8 of the 72 bytes per frame less
-        legs["c2_64B_1flow_multiburst_rec8"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed,
-                                                              rec=rxg.REC8)
+        legs["c2_64B_1flow_multiburst"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed,
+                                                         rec=args.rec)
+        # the other record kind on the same ring and on the headline workload (16 <-> 8 bytes)
+        other = rxg.REC16 if args.rec == rxg.REC8 else rxg.REC8
+        legs[f"c2_64B_1flow_multiburst_rec{other}"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device,
+                                                                     seed, rec=other)
+        ow = Workload(eng, args.workload, frames, seed, other)
+        eng.tcb_load(tcb, live)
+        _, ko = time_workload(eng, ow, args.steps, args.warmup, device, stream)
+        ka = max_over_ranks(float(np.mean(ko)) / 1e3, device)
+        legs[f"{args.workload}_rec{other}"] = {"kernel_us": round(ka * 1e6, 2),
+                                               "roofline_frac": round(ow.bytes_per_batch / ka / 1e9 / HBM_PEAK_GBS, 4)}
+        ow.free()
         legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
         legs["tx_generate_dev"] = tx_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)

@@ -2,7 +2,7 @@
 """A fixed number of rx launches of one bench workload through the product library, for
 rocprofv3 (kernel trace / PMC passes): scripts/gpu_prof.sh.  The same synthetic batches,
 tables and launch forms as bench.py; no timing of its own.
-  python scripts/profrun.py --workload c2multi --iters 20"""
+  python scripts/profrun.py --workload c2multi --iters 20 [--rec 8]"""
 import argparse
 import os
 import sys
@@ -22,27 +22,29 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WL) + ["c2multi"])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--rec", type=int, default=16, choices=[8, 16, 48])
     args = ap.parse_args()
+    rec = args.rec
     eng = rxg.Engine(0)
     n = args.frames
     if args.workload == "c2multi":  # bench.py multiburst_leg: 16 bursts of one 1 GiB pool per launch
         k = 16
         pool = eng.synth(n=n * k, nflows=1, len_a=64, mix=0, seed=0x5EED0001 + 123)
         eng.tcb_load(*rxg.synthetic_tcb_table(1))
-        out = eng.alloc(n * k * 16)
-        bursts = [(pool["off64"].ptr + j * n * 4, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * 16)
+        out = eng.alloc(n * k * rec)
+        bursts = [(pool["off64"].ptr + j * n * 4, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * rec)
                   for j in range(k)]
         for _ in range(args.iters):
-            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rxg.REC16)
+            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
         eng.sync()
         return
     L, flows, mix, copies = WL[args.workload]
     bs = [eng.synth(n=n, nflows=flows, len_a=L or 1500, mix=mix, seed=0x5EED0001 + 17 * c) for c in range(copies)]
     eng.tcb_load(*rxg.synthetic_tcb_table(flows))
-    out = eng.alloc(n * 16)
+    out = eng.alloc(n * rec)
     for i in range(args.iters):
         b = bs[i % copies]
-        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, out.ptr, rxg.REC16)
+        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, out.ptr, rec)
     eng.sync()
 
 
