@@ -255,7 +255,7 @@ extern "C" int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32
 }
 
 extern "C" int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, void *const *mbufs,
-                                   void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t stride)
+                                   void *const *frames, const void *recs, uint32_t n, uint32_t stride)
 {
     if (!g || !ops || (n && (!mbufs || !frames || !recs))) return gfail(-EINVAL, "rxg_group_rx_replay: NULL argument");
     if (n != g->last_n) return gfail(-EINVAL, "rxg_group_rx_replay: n=%u but the last group burst had %u", n, g->last_n);
@@ -283,7 +283,7 @@ extern "C" int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, voi
         // the member's mirror already holds every write the earlier shards' handlers made
         // (they went through rxg_group_tcb_*); its replay re-classifies what they affect
         const int rc = rxg_rx_replay(g->m[i], &so, mbufs + o, frames + o,
-                                     (const rxg_rec16 *)((const uint8_t *)recs + (size_t)o * stride), g->shard_n[i],
+                                     (const uint8_t *)recs + (size_t)o * stride, g->shard_n[i],
                                      stride);
         if (rc) return gfail(rc, "member %zu: %s", i, rxg_last_error());
     }

@@ -1027,7 +1027,7 @@ static constexpr uint32_t kHostReclassifyMax = 256;
 
 // The side effects of etherin.c:21-35, ip.c:26-39 and tcp_in.c:47-72, in packet order.
 extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const *mbufs,
-                             void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t stride)
+                             void *const *frames, const void *recs, uint32_t n, uint32_t stride)
 {
     if (!c || !ops || (n && (!mbufs || !frames || !recs)))
         return fail(-EINVAL, "rxg_rx_replay: NULL argument");

@@ -160,7 +160,7 @@ int main(int argc, char **argv)
     g_out = calloc(n, sizeof *g_out);
     for (uint32_t i = 0; i < n; ++i) g_out[i].tcb_idx = -1;
     rxg_pkt_view *views = calloc(burst, sizeof *views);
-    rxg_rec16 *recs = calloc(burst, sizeof *recs);
+    rxg_rec8 *recs = calloc(burst, sizeof *recs); /* 8-byte records: all the replay reads */
     void **mbufs = calloc(burst, sizeof *mbufs), **frames = calloc(burst, sizeof *frames);
     rxg_handoff_ops ops = {.free_mbuf = ops_free,
                            .send_reset = ops_rst,
@@ -179,8 +179,8 @@ int main(int argc, char **argv)
             mbufs[i] = (void *)(uintptr_t)(b0 + i + 1);
             frames[i] = g_frames[b0 + i];
         }
-        if (rxg_rx_burst(g_rxg, views, nb, RXG_REC16, recs) != 0 ||
-            rxg_rx_replay(g_rxg, &ops, mbufs, frames, recs, nb, RXG_REC16) != 0) {
+        if (rxg_rx_burst(g_rxg, views, nb, RXG_REC8, recs) != 0 ||
+            rxg_rx_replay(g_rxg, &ops, mbufs, frames, recs, nb, RXG_REC8) != 0) {
             fprintf(stderr, "rx: %s\n", rxg_last_error());
             return 3;
         }

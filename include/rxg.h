@@ -419,10 +419,12 @@ typedef struct rxg_handoff_ops {
    replayed, and the counters are corrected.  The composition rxg_rx_burst + rxg_rx_replay
    therefore equals `for (i<n) ether_in(mbufs[i])`.  After rxg_rx_bursts_dev the launch's
    bursts are replayed in order, one call each, and their composition equals ether_in over
-   their concatenation.  -EINVAL when n differs from the burst to be replayed or the launch
-   failed after it started (nothing is replayed then). */
+   their concatenation.  recs: the burst's records as the launch wrote them, rec_stride =
+   their kind (RXG_REC8: rxg_rec8[], RXG_REC16: rxg_rec16[], RXG_REC48: rxg_rec48[]).
+   -EINVAL when n differs from the burst to be replayed or the launch failed after it started
+   (nothing is replayed then). */
 int rxg_rx_replay(rxg_ctx *ctx, const rxg_handoff_ops *ops, void *const *mbufs,
-                  void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
+                  void *const *frames, const void *recs, uint32_t n, uint32_t rec_stride);
 
 /* Cumulative replay statistics of the context: out[0] packets marked stale by in-burst
    table writes, out[1] of them re-classified from the host index, out[2] re-classified on
@@ -595,7 +597,7 @@ int rxg_group_rcv_set(rxg_group *g, int32_t idx, uint32_t cur_seq, uint32_t pair
 int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32_t n, uint32_t rec_kind,
                        void *out_host);
 int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, void *const *mbufs,
-                        void *const *frames, const rxg_rec16 *recs, uint32_t n, uint32_t rec_stride);
+                        void *const *frames, const void *recs, uint32_t n, uint32_t rec_stride);
 /* rxg_payload_take on the member whose shard is being replayed (0 outside a replay);
    each member's rxg_payload_gather_dev covers its own shard. */
 int rxg_group_payload_take(rxg_group *g, int32_t idx, uint32_t seq, uint32_t length, rxg_payload_msg *msg);

@@ -55,19 +55,21 @@ def test_group_burst_equals_single_context(engine, ndev):
         assert len(g) == ndev
         g.tcb_load(tcb, live)
         g.counters_reset()
-        for kind in (rxg.REC48, rxg.REC16):
+        for kind in (rxg.REC48, rxg.REC16, rxg.REC8):
             recs = g.rx_burst(frames, kind)
-            want = single if kind == rxg.REC48 else np.ascontiguousarray(single["c"])
+            want = {rxg.REC48: single, rxg.REC16: np.ascontiguousarray(single["c"]),
+                    rxg.REC8: rxg.rec8_pack(single["c"])}[kind]
             assert recs.tobytes() == want.tobytes()
-        assert g.counters().tolist() == (2 * scnt).tolist()
+        assert g.counters().tolist() == (3 * scnt).tolist()
         # fewer frames than members: empty shards are bursts of nothing
         one = g.rx_burst(frames[:1], rxg.REC48)
         assert one.tobytes() == single[:1].tobytes()
         assert len(g.rx_burst([], rxg.REC48)) == 0
 
 
-@pytest.mark.parametrize("ndev,seed", [(2, 1), (3, 2), (2, 3)])
-def test_group_replay_sequential_equivalence(ndev, seed):
+@pytest.mark.parametrize("ndev,seed,kind", [(2, 1, rxg.REC16), (3, 2, rxg.REC16), (2, 3, rxg.REC16),
+                                            (3, 4, rxg.REC8)])
+def test_group_replay_sequential_equivalence(ndev, seed, kind):
     """Handlers write through the group, so a write made while replaying shard i reaches the
     members of shards i+1.. before their replay, which re-classifies what it affects."""
     rows, frames = scenario(seed)
@@ -76,13 +78,13 @@ def test_group_replay_sequential_equivalence(ndev, seed):
     with rxg.Group([0] * ndev, **MB) as g:
         g.tcb_load(tcb, live)
         g.counters_reset()
-        recs = g.rx_burst(frames, rxg.REC16)
+        recs = g.rx_burst(frames, kind)
         model = Model(rows, g)
         bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
         got = [None] * len(frames)
         ops = _ops(frames, bufs, got, model)
         ptrs = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
-        g.rx_replay(ops, ptrs, ptrs, recs.ctypes.data, len(bufs), 16)
+        g.rx_replay(ops, ptrs, ptrs, recs.ctypes.data, len(bufs), kind)
         for i, (v, idx, st) in enumerate(exp):
             if v == rxg.V_DISPATCH:
                 assert got[i] == ("switch", idx, st), (i, got[i], exp[i])
