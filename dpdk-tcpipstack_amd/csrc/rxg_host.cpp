@@ -136,6 +136,9 @@ struct rxg_ctx {
     std::vector<uint32_t> rcv_cur;
     std::vector<uint8_t> rcv_state;
     DevBuf d_pg_status, d_pg_ticket;
+#ifdef RXG_EXPERIMENTS
+    DevBuf d_exp_hdr;  // RXG_VARIANT 21: contiguous header lines of a tx batch
+#endif
     unsigned long long pg_tickets = 0;  // workgroups the gathers have launched so far
     uint32_t pg_epoch = 0;
     rxg_payload_msg *h_pm = nullptr;
@@ -289,6 +292,9 @@ extern "C" int rxg_fini(rxg_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket})
         if (b->p) (void)hipFree(b->p);
+#ifdef RXG_EXPERIMENTS
+    if (c->d_exp_hdr.p) (void)hipFree(c->d_exp_hdr.p);
+#endif
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
     if (c->h_patch) (void)hipHostFree(c->h_patch);
@@ -690,7 +696,13 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
         return fail(-EINVAL, "rxg_tx_cksum_dev: NULL device pointer");
     int rc = set_device(c);
     if (rc) return rc;
-    const LaunchBurst one{b->off64, b->len, b->n, nullptr};
+    LaunchBurst one{b->off64, b->len, b->n, nullptr};
+#ifdef RXG_EXPERIMENTS
+    if (c->variant == 21) {
+        if ((rc = ensure(c->d_exp_hdr, (size_t)b->n * 64u))) return rc;
+        one.out = (uint8_t *)c->d_exp_hdr.p;
+    }
+#endif
     LaunchRx L;
     std::memset(&L, 0, sizeof L);
     L.frames = (const uint8_t *)b->frames;

@@ -552,7 +552,7 @@ __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32
     return F;
 }
 
-template <int C, int LPF, int NLOAD, int MODE, bool NT, bool NTSTORE = false>
+template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV = 0>
 __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                    int lane)
 {
@@ -677,10 +677,14 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
                 uint4 q = make_uint4(d[j][0], d[j][1], d[j][2], d[j][3]);
                 if (c == 1) q.z = (q.z & 0xFFFF0000u) | (ck2 & 0xFFFFu);        // bytes 24-25
                 if (c == 3) q.x = (q.x & 0x0000FFFFu) | (ck2 & 0xFFFF0000u);    // bytes 50-51
-                if constexpr (NTSTORE) {  // experiment build only (RXG_VARIANT 20)
+                if constexpr (SV == 1) {  // experiment build only (RXG_VARIANT 20)
                     u32x4 v;
                     v.x = q.x; v.y = q.y; v.z = q.z; v.w = q.w;
                     __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(fp + 16 * c));
+                } else if constexpr (SV == 2) {
+                    // experiment build only (RXG_VARIANT 21, uniform 1 536 B slots): the
+                    // line goes to a contiguous array of header lines, frame off / 24
+                    *reinterpret_cast<uint4 *>(a.b[0].out + (size_t)(off / 24u) * 64u + 16 * c) = q;
                 } else {
                     *reinterpret_cast<uint4 *>(fp + 16 * c) = q;
                 }
@@ -690,7 +694,7 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
     return F;
 }
 
-template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool NTSTORE = false>
+template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int SV = 0>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
                                           int lane_in, uint32_t *sf)
 {
@@ -733,7 +737,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             load_chunks<1, 4, NT>(a, koff, act ? klen : 0u, act, rl, d);
             F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
         } else if constexpr (LPF >= 2 && !JUMBO)
-            F = frame_round_fast<C, LPF, NLOAD, MODE, NT, NTSTORE>(a, act ? koff : 0u, act ? klen : 0u, act, rl);
+            F = frame_round_fast<C, LPF, NLOAD, MODE, NT, SV>(a, act ? koff : 0u, act ? klen : 0u, act, rl);
         else
             F = frame_round<LPF, NLOAD, JUMBO, MODE, NT>(a, koff, act ? klen : 0u, act, rl);
         if constexpr (MODE != 0) {
@@ -1241,12 +1245,12 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, (STRIP & 64) != 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT, (STRIP & 64) != 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, (STRIP & 64) != 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, (STRIP & 64) != 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, (STRIP & 64) != 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, (STRIP & 64) != 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 7) & 1) run_class<7, 64, 2, true, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr (MODE == 0 || (STRIP & 8)) {
             wcount(wc, RXG_C_RX, valid);
@@ -1477,6 +1481,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
 #ifdef RXG_EXPERIMENTS
         if (L.variant == 20)  // non-temporal stores of the rewritten header lines
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 64>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 21)  // header lines stored to a contiguous array (C3 frames only)
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 128>), dim3(blocks), dim3(256), 0, st, a);
         else
 #endif
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
