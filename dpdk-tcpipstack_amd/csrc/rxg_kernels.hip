@@ -819,6 +819,34 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr, fc, cached);
 }
 
+// Deferred phase B (DEFER kernels): the first bucket of each lane's probe is loaded by
+// LDS-DMA (global_load_lds_dwordx4, no VGPR destination) into the wave's 4 KiB probe
+// buffer pb[k][lane] while the next slice streams; classify_finish runs one slice later.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ __forceinline__ uint32_t probe_bucket(const RxArgs &a, const Fields &F)
+{
+    return tuple_hash(F.ports, F.dst, bswap32(F.src)) & a.t.bucket_mask;
+}
+
+__device__ __forceinline__ void probe_issue_lds(const RxArgs &a, const Fields &F, uint4 (*pb)[64])
+{
+    const uint4 *b = a.t.buckets + (size_t)probe_bucket(a, F) * kSlotsPerBucket;
+#pragma unroll
+    for (int k = 0; k < kSlotsPerBucket; ++k)
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(b + k), (lds_void_t *)&pb[k][0], 16, 0, 0);
+}
+
+__device__ __forceinline__ Probe probe_from_lds(const RxArgs &a, const Fields &F, const uint4 (*pb)[64], int lane)
+{
+    Probe P;
+    P.hb = probe_bucket(a, F);
+#pragma unroll
+    for (int k = 0; k < kSlotsPerBucket; ++k) P.s[k] = pb[k][lane];
+    return P;
+}
+
 template <int MODE, int STRIP>
 __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
                                                 const Fields &F, const Probe &P, WaveCounters &wc,
@@ -1174,21 +1202,23 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     return nxt;
 }
 
-template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false>
+template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 8, bool MULTI = false,
+          bool DEFER = false, bool DTOP = true>
 __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 {
+    static_assert(!DEFER || MODE == 8 || MODE == 16, "deferred phase B: REC8 / REC16 only");
     constexpr int NF = MODE == 48 ? NF48 : NF16;
     __shared__ unsigned long long s_cnt[4][RXG_NCOUNTERS];
-    // Per-wave LDS = the record ring (REC16: RS16 = 11 slices of 1 KiB, REC48: 4 of 3 KiB,
-    // 3 workgroups per CU: the best of 2-5 per CU over C2, C3, C4); its
-    // free slots are also the scratch of the slice in progress (4 KiB small-slice transpose,
-    // NF x 256 B parked fields), so LDS per wave is the ring alone and sets the occupancy.
-    // REC8: 22 slots of 512 B (the same 11 KiB per wave as REC16's ring)
+    // Per-wave LDS = the record ring (REC16: RS16 = 8 slices of 1 KiB, REC8: 16 of 512 B,
+    // REC48: 4 of 3 KiB); its free slots are also the scratch of the slice in
+    // progress (4 KiB small-slice transpose, NF x 256 B parked fields), so LDS per wave is
+    // the ring alone.  At 148 VGPRs the kernel runs 3 waves per SIMD, 3 workgroups per CU.
     constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : MODE == 8 ? 2 * RS16 : 1;
     constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE);
     static_assert(MODE == 0 || RS * kSlot * 16 >= 4096 + kSlot * 16, "ring too small for the scratch");
     __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kSlot];
     __shared__ uint32_t s_recf[4][RS];
+    __shared__ __attribute__((aligned(16))) uint4 s_pb[DEFER ? 4 : 1][kSlotsPerBucket][DEFER ? 64 : 1];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
@@ -1212,8 +1242,29 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     BurstCursor<MULTI> bc;
     bc.load(a, lane);
     load_desc<SEL>(a, s, lane, c_off, c_len, bc);
-    load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+    if constexpr (!DTOP) load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+    // DEFER: the slice whose phase B is pending (wave-uniform; ~0 = none), its fields
+    uint32_t d_s = ~0u, d_len = 0u;
+    bool d_cached = true;
+    Fields dF{};
+    auto finish_pending = [&]() {
+        if constexpr (DEFER) {
+            if (d_s == ~0u) return;
+            const bool dvalid = (uint32_t)lane < slice_frames(a, uniform(d_s), bc);
+            const Probe P = d_cached ? probe_none() : probe_from_lds(a, dF, s_pb[wid], lane);
+            classify_finish<MODE, STRIP>(a, d_s * 64u + (uint32_t)lane, dvalid, d_len, dF, P, wc, rec, fcache,
+                                         d_cached);
+            if (ring.n == RS) ring.flush(a, lane, bc);
+            ring.put(d_s, lane, rec);
+            d_s = ~0u;
+        }
+    };
     while (s < nslices) {
+        // DTOP: the next slice's descriptors are loaded as this slice starts.  Loaded at the
+        // slice's end instead (two slices ahead), they were still in flight at the loop's
+        // back edge, where the register copy c <- n made the wave wait for them (an
+        // s_waitcnt vmcnt(0) per slice in the ISA); C4 81.0 -> 79.2 us.
+        if constexpr (DTOP) load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
         const uint32_t f = s * 64u + (uint32_t)lane;
         const bool valid = (uint32_t)lane < slice_frames(a, uniform(s), bc);
         const uint32_t off = c_off, len = valid ? c_len : 0u;
@@ -1227,6 +1278,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
                 // slice's frames) and every wait leaves the next slice's frames in flight.
                 // The two frame buffers alternate between the unrolled steps P = 0, 1 (a
                 // register copy of a load in flight would wait for it).
+                finish_pending();
                 uint4 vb[2][4];
                 issue_small_slice<true>(a, c_off, c_len, lane, vb[0]);
                 for (;;) {
@@ -1254,6 +1306,22 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         if constexpr ((CMASK >> 7) & 1) run_class<7, 64, 2, true, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr (MODE == 0 || (STRIP & 8)) {
             wcount(wc, RXG_C_RX, valid);
+        } else if constexpr (DEFER) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const Fields F = unpark_fields<MODE>(sf, lane);
+            // the previous slice's phase B (its probe landed while this slice streamed); its
+            // record may go to the slot this slice's fields were parked in: they are read
+            finish_pending();
+            const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
+            const bool is_tcp = valid && et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
+            d_cached = __ballot(is_tcp && !fc_hit(fcache, F)) == 0ull;
+            if (!d_cached) probe_issue_lds(a, F, s_pb[wid]);
+            d_s = s;
+            d_len = len;
+            dF = F;
+            __builtin_amdgcn_wave_barrier();  // reads before the next slice's writes
         } else {
             // the fields parked by other lanes of this wave must be visible to this lane
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1268,8 +1336,9 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         }
         s += nwaves;
         c_off = n_off; c_len = n_len;
-        load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+        if constexpr (!DTOP) load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
     }
+    finish_pending();
     if constexpr (MODE != 0) ring.flush(a, lane, bc);
 
     if (a.counters == nullptr) return;
@@ -1455,26 +1524,48 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 12: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         case 13: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 8>), dim3(blocks), dim3(256), 0, st, a); break;
         case 14: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 16>), dim3(blocks), dim3(256), 0, st, a); break;
+        // deferred phase B (probe by LDS-DMA, classified one slice later): 30 with an 8-slot
+        // ring (3 workgroups per CU), 31 with the 11-slot ring (2 per CU); 32 = 8-slot ring alone
+        case 30: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 31: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
+        // 32: the round-2 start (11-slot ring, next descriptors loaded at the slice's end);
+        // 40: descriptors at the slice's start with the 11-slot ring
+        case 32: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 40: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
             if (a.nbursts > 1)
-                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
             else
                 hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
 #else
         if (a.nbursts > 1)
-            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
 #endif
     } else if (L.mode == 8) {
+#ifdef RXG_EXPERIMENTS
+        if (L.variant == 30 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, true>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 40 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, true>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 32 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+#endif
         if (a.nbursts > 1)
-            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (L.mode == 48) {
         if (a.nbursts > 1)
-            hipLaunchKernelGGL((rx_kernel<48, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((rx_kernel<48, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<48, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     } else {
@@ -1483,6 +1574,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 64>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 21)  // header lines stored to a contiguous array (C3 frames only)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 128>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 32)  // descriptors loaded at the slice's end (round-2 start)
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
         else
 #endif
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
