@@ -1178,10 +1178,13 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     // both in flight.  (Probe after the frames: the probe's wait drained the prefetch,
     // 64 B / 64 K flows 28.4 us.)
     const uint32_t s1 = s + nwaves;
-    const bool nxt = s1 < nslices && slice_frames(a, uniform(s1), bc) == 64u && __ballot(n_len <= 64u) == ~0ull;
     uint32_t d[4][4];
     uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
     transpose_small_slice(vb[P], lane, sf, d);
+    // the next slice's descriptors are read after this slice's frames have landed: they were
+    // issued before them (loop top) or just after (previous step), so this waits for no
+    // more than the frames did
+    const bool nxt = s1 < nslices && slice_frames(a, uniform(s1), bc) == 64u && __ballot(n_len <= 64u) == ~0ull;
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
@@ -1202,17 +1205,17 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     return nxt;
 }
 
-template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 8, bool MULTI = false,
+template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
           bool DEFER = false, bool DTOP = true>
 __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
 {
     static_assert(!DEFER || MODE == 8 || MODE == 16, "deferred phase B: REC8 / REC16 only");
     constexpr int NF = MODE == 48 ? NF48 : NF16;
     __shared__ unsigned long long s_cnt[4][RXG_NCOUNTERS];
-    // Per-wave LDS = the record ring (REC16: RS16 = 8 slices of 1 KiB, REC8: 16 of 512 B,
+    // Per-wave LDS = the record ring (REC16: RS16 = 11 slices of 1 KiB, REC8: 22 of 512 B,
     // REC48: 4 of 3 KiB); its free slots are also the scratch of the slice in
     // progress (4 KiB small-slice transpose, NF x 256 B parked fields), so LDS per wave is
-    // the ring alone.  At 148 VGPRs the kernel runs 3 waves per SIMD, 3 workgroups per CU.
+    // the ring alone.  3 workgroups per CU (LDS and, at ~145 VGPRs, registers).
     constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : MODE == 8 ? 2 * RS16 : 1;
     constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE);
     static_assert(MODE == 0 || RS * kSlot * 16 >= 4096 + kSlot * 16, "ring too small for the scratch");
@@ -1242,7 +1245,7 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
     BurstCursor<MULTI> bc;
     bc.load(a, lane);
     load_desc<SEL>(a, s, lane, c_off, c_len, bc);
-    if constexpr (!DTOP) load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+    load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
     // DEFER: the slice whose phase B is pending (wave-uniform; ~0 = none), its fields
     uint32_t d_s = ~0u, d_len = 0u;
     bool d_cached = true;
@@ -1260,11 +1263,6 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         }
     };
     while (s < nslices) {
-        // DTOP: the next slice's descriptors are loaded as this slice starts.  Loaded at the
-        // slice's end instead (two slices ahead), they were still in flight at the loop's
-        // back edge, where the register copy c <- n made the wave wait for them (an
-        // s_waitcnt vmcnt(0) per slice in the ISA); C4 81.0 -> 79.2 us.
-        if constexpr (DTOP) load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
         const uint32_t f = s * 64u + (uint32_t)lane;
         const bool valid = (uint32_t)lane < slice_frames(a, uniform(s), bc);
         const uint32_t off = c_off, len = valid ? c_len : 0u;
@@ -1293,6 +1291,12 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
             }
         }
         bytes += len;
+        // Descriptors two slices ahead.  DTOP: loaded as the class-path slice starts, so
+        // they have landed by the loop's back edge.  Loaded at the slice's end instead, they
+        // were still in flight there, where the register copies c <- n <- y made the wave
+        // wait for them (an s_waitcnt vmcnt(0) per slice in the ISA).
+        uint32_t y_off = 0u, y_len = 0u;
+        if constexpr (DTOP) load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
         uint32_t *sf = MODE == 0 ? nullptr : ring.scratch(a, lane, NF * 256, bc);
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
@@ -1336,7 +1340,11 @@ __global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
         }
         s += nwaves;
         c_off = n_off; c_len = n_len;
-        if constexpr (!DTOP) load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+        if constexpr (DTOP) {
+            n_off = y_off; n_len = y_len;
+        } else {
+            load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+        }
     }
     finish_pending();
     if constexpr (MODE != 0) ring.flush(a, lane, bc);
@@ -1528,19 +1536,25 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         // ring (3 workgroups per CU), 31 with the 11-slot ring (2 per CU); 32 = 8-slot ring alone
         case 30: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 31: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
-        // 32: the round-2 start (11-slot ring, next descriptors loaded at the slice's end);
-        // 40: descriptors at the slice's start with the 11-slot ring
-        case 32: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a); break;
-        case 40: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
+        // 32: the round-2 start (descriptors two slices ahead loaded at the slice's end);
+        // 33: the same with an 8-slot ring; 41: production with an 8-slot ring
+        case 32:
+            if (a.nbursts > 1)
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true, false, false>), dim3(blocks), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
+            break;
+        case 41: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 33: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, false>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
             if (a.nbursts > 1)
-                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
             else
                 hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
 #else
         if (a.nbursts > 1)
-            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
 #endif
@@ -1550,22 +1564,29 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, true>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
-        if (L.variant == 40 && a.nbursts == 1) {
-            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, true>), dim3(blocks), dim3(256), 0, st, a);
+        if (L.variant == 41 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, false, true>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
-        if (L.variant == 32 && a.nbursts == 1) {
-            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
+        if (L.variant == 33 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 32) {
+            if (a.nbursts > 1)
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, true, false, false>), dim3(blocks), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
 #endif
         if (a.nbursts > 1)
-            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (L.mode == 48) {
         if (a.nbursts > 1)
-            hipLaunchKernelGGL((rx_kernel<48, 0xFF, true, 0, false, 8, true>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((rx_kernel<48, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<48, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
     } else {

@@ -22,7 +22,10 @@ import rxg  # noqa: E402
 WL = {"c3": (1500, 1000, 0, 1), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3),
       "c2r1": (64, 1, 0, 1), "c2x4": (64, 1, 0, 4),
       # single-size legs of the IMIX (64 K flows): where C4's time goes
-      "u64": (64, 65536, 0, 16), "u576": (576, 65536, 0, 2), "u1500": (1500, 65536, 0, 1)}
+      "u64": (64, 65536, 0, 16), "u576": (576, 65536, 0, 2), "u1500": (1500, 65536, 0, 1),
+      # C2 as 16 bursts of one 1 GiB pool per launch (rxg_rx_bursts_dev, bench.py multiburst_leg)
+      "c2m": (64, 1, 0, 1)}
+MULTI = 16
 
 
 def main():
@@ -42,12 +45,18 @@ def main():
     for w in args.workloads.split(","):
         L, flows, mix, copies = WL[w]
         nfr = args.frames_c2 if (w.startswith("c2") and args.frames_c2) else args.frames
+        if w == "c2m":  # one pool of MULTI bursts; the workload's bytes are the whole launch's
+            pool = base.synth(n=nfr * MULTI, nflows=1, len_a=64, mix=0, seed=77)
+            tcb, live = rxg.synthetic_tcb_table(1)
+            wls[w] = ([pool], nfr * MULTI * 64, tcb, live, nfr)
+            continue
         bs = [base.synth(n=nfr, nflows=flows, len_a=L or 1500, mix=mix, seed=77 + c)
               for c in range(copies)]
         lens = bs[0]["len"].download(np.uint16, nfr)
         tcb, live = rxg.synthetic_tcb_table(flows)
         wls[w] = (bs, int(lens.astype(np.uint64).sum()), tcb, live, nfr)
-    out = base.alloc(max(args.frames, args.frames_c2) * args.rec)
+    nout = max(args.frames, args.frames_c2) * (MULTI if "c2m" in wls else 1)
+    out = base.alloc(nout * args.rec)
     base.sync()
 
     # A variant may name another build of librxg (4th field, a path): A/B of two builds in
@@ -78,7 +87,11 @@ def main():
                 eng.tcb_sync()
                 evs = [(eng.event(), eng.event()) for _ in range(args.iters)]
                 def launch(b):
-                    if args.tx:  # the batch's checksums are already right: rewriting keeps them
+                    if w == "c2m":
+                        R = args.rec
+                        eng.rx_bursts_dev(b["arena"].ptr, [(b["off64"].ptr + j * nfr * 4, b["len"].ptr + j * nfr * 2,
+                                                            nfr, out.ptr + j * nfr * R) for j in range(MULTI)], R)
+                    elif args.tx:  # the batch's checksums are already right: rewriting keeps them
                         eng.tx_cksum_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, nfr)
                     else:
                         eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, nfr, out.ptr, args.rec)
