@@ -1206,8 +1206,8 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
 }
 
 template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
-          bool DEFER = false, bool DTOP = true>
-__global__ __launch_bounds__(256) void rx_kernel(RxArgs a)
+          bool DEFER = false, bool DTOP = true, int WPE = 1>
+__global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
 {
     static_assert(!DEFER || MODE == 8 || MODE == 16, "deferred phase B: REC8 / REC16 only");
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -1546,6 +1546,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             break;
         case 41: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 33: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, false>), dim3(blocks), dim3(256), 0, st, a); break;
+        // 4 waves per SIMD (at most 128 VGPRs) with the 8-slot ring (4 workgroups per CU fit in LDS)
+        case 34: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
             if (a.nbursts > 1)
                 hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
@@ -1566,6 +1568,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 41 && a.nbursts == 1) {
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, false, true>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 34 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 33 && a.nbursts == 1) {
