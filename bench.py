@@ -54,7 +54,7 @@ def traffic_of(name, n, rec):
     return None, None
 WORKLOADS = {
     # name: (frame_len, flows, mix, rotating copies)
-    "c3_1500B_1Kflows": (1500, 1000, 0, 1),
+    "c3_1500B_1Kflows": (1500, 1000, 0, 2),  # 2 rotating 1.5 GiB batches: no step re-reads the last one's tail from the 256 MB MALL
     "c2_64B_1flow": (64, 1, 0, 16),
     "c4_imix_64Kflows": (0, 65536, 1, 3),
 }

@@ -19,7 +19,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")]
 os.environ.setdefault("RXG_LIB", os.path.join(ROOT, "dpdk-tcpipstack_amd", "rxg", "librxg_exp.so"))
 import rxg  # noqa: E402
 
-WL = {"c3": (1500, 1000, 0, 1), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3),
+WL = {"c3": (1500, 1000, 0, 2), "c3r1": (1500, 1000, 0, 1), "c4r4": (0, 65536, 1, 4), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3),
       "c2r1": (64, 1, 0, 1), "c2x4": (64, 1, 0, 4),
       # single-size legs of the IMIX (64 K flows): where C4's time goes
       "u64": (64, 65536, 0, 16), "u576": (576, 65536, 0, 2), "u1500": (1500, 65536, 0, 1),

@@ -14,7 +14,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")]
 import rxg  # noqa: E402
 
 # name: (frame_len, flows, mix, rotating copies) -- bench.py WORKLOADS
-WL = {"c3": (1500, 1000, 0, 1), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3)}
+WL = {"c3": (1500, 1000, 0, 2), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3)}
 
 
 def main():
