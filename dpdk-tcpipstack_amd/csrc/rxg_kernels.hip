@@ -670,10 +670,13 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
         // (C3 tx 327 -> 310 us; holding the writes until the next round's loads are
         // issued measured slower, 322).
         const uint32_t ck2 = lane_read(bswap16(ip_ck) | (bswap16(tcp_ck) << 16), gbase);
+        // SV 3 (experiment build only, RXG_VARIANT 22): the whole first 128-byte line (an L2
+        // line) is rewritten where the frame covers it, not only the first 64 bytes
+        constexpr int kLineChunks = SV == 3 ? 8 : 4;
 #pragma unroll
-        for (int j = 0; j < NLOAD && j * LPF < 4; ++j) {
+        for (int j = 0; j < NLOAD && j * LPF < kLineChunks; ++j) {
             const int c = gl + j * LPF;
-            if (active && c < 4) {
+            if (active && (c < 4 || (c < kLineChunks && (uint32_t)(c + 1) * 16u <= len))) {
                 uint4 q = make_uint4(d[j][0], d[j][1], d[j][2], d[j][3]);
                 if (c == 1) q.z = (q.z & 0xFFFF0000u) | (ck2 & 0xFFFFu);        // bytes 24-25
                 if (c == 3) q.x = (q.x & 0x0000FFFFu) | (ck2 & 0xFFFF0000u);    // bytes 50-51
@@ -1301,12 +1304,12 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : 0>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 7) & 1) run_class<7, 64, 2, true, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr (MODE == 0 || (STRIP & 8)) {
             wcount(wc, RXG_C_RX, valid);
@@ -1601,6 +1604,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 64>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 21)  // header lines stored to a contiguous array (C3 frames only)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 128>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 22)  // whole 128-byte first lines rewritten
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 256>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 32)  // descriptors loaded at the slice's end (round-2 start)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
         else
