@@ -1240,14 +1240,10 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
     if (c->replay_cursor + 1 < c->last_bursts.size()) select_burst(c, c->replay_cursor + 1);
     bool nz = false;
     for (int k = 0; k < RXG_NCOUNTERS; ++k) nz |= delta[k] != 0;
-    if (nz) {  // add the corrections to the host row of the counter block
-        uint64_t row[RXG_NCOUNTERS];
-        unsigned long long *dst = c->counters + (size_t)(RXG_COUNTER_ROWS - 1) * RXG_NCOUNTERS;
-        HIP_OK(hipMemcpyAsync(row, dst, sizeof row, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
-        for (int k = 0; k < RXG_NCOUNTERS; ++k) row[k] += (uint64_t)delta[k];
-        HIP_OK(hipMemcpyAsync(dst, row, sizeof row, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
+    if (nz) {  // add the corrections to the host row of the counter block, in stream order
+        CounterDelta d;
+        for (int k = 0; k < RXG_NCOUNTERS; ++k) d.v[k] = delta[k];
+        HIP_OK(launch_counters_add(c->counters + (size_t)(RXG_COUNTER_ROWS - 1) * RXG_NCOUNTERS, d, c->stream));
     }
     return 0;
 }

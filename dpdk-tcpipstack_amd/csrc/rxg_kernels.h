@@ -65,6 +65,12 @@ int rx_blocks_per_cu(int mode);
 hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);
 // rxg_mirror.h patches (n of them, host-visible memory) applied to the device mirror tables
 struct MirrorPatch;
+// Replay counter corrections (two's complement: a negative delta wraps the uint64 sum)
+struct CounterDelta {
+    int64_t v[RXG_NCOUNTERS];
+};
+hipError_t launch_counters_add(unsigned long long *row, const CounterDelta &d, hipStream_t st);
+
 hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets, int32_t *listen, uint2 *arp,
                                hipStream_t st);
 

@@ -1640,6 +1640,21 @@ hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets,
     return hipGetLastError();
 }
 
+// The replay's counter corrections (rxg_rx_replay), added to the host row of the counter
+// block in stream order: the values travel as kernel arguments, so the host neither waits
+// for nor reads back the device block.
+__global__ void counters_add(unsigned long long *row, CounterDelta d)
+{
+    const int k = (int)threadIdx.x;
+    if (k < RXG_NCOUNTERS && d.v[k] != 0) atomicAdd(row + k, (unsigned long long)d.v[k]);
+}
+
+hipError_t launch_counters_add(unsigned long long *row, const CounterDelta &d, hipStream_t st)
+{
+    hipLaunchKernelGGL(counters_add, dim3(1), dim3(64), 0, st, row, d);
+    return hipGetLastError();
+}
+
 int rx_blocks_per_cu(int mode)
 {
     int n = 0;
