@@ -708,6 +708,9 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
     return F;
 }
 
+__device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int lane, uint32_t *sf,
+                                                      uint32_t (&d)[4][4]);
+
 template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int SV = 0>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
                                           int lane_in, uint32_t *sf)
@@ -746,7 +749,25 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
         int rl = lane;
         asm volatile("" : "+v"(rl));  // keep per-round lane math inside the round (VGPRs)
         Fields F;
-        if constexpr (LPF == 1) {
+        if constexpr (LPF == 1 && MODE != 0 && SV != 6) {
+            // The class's frames are loaded as the all-small path loads a slice (lane l:
+            // chunk l&3 of frame 16j + l/4, 16 whole frames and 16 lines per instruction) and
+            // transposed through LDS (4 KiB after the parked fields).  Lane i loading its own
+            // frame's four chunks touched up to 64 lines per instruction: C4 78.9 -> 75.2 us
+            // (SV 6 = that form, experiment variant 26).
+            uint4 v[4];
+            const int ch = rl & 3;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int fr = 16 * j + (rl >> 2);
+                const uint32_t foff = lane_read(coff, fr), flen = lane_read(clen, fr);
+                const bool ok = (uint32_t)fr < cnt && (uint32_t)(ch * 16) < flen;
+                v[j] = load16<NT>(ok ? a.frames + (size_t)foff * 64u + ch * 16 : a.frames);
+            }
+            uint32_t d[4][4];
+            transpose_small_slice(v, rl, sf + (MODE == 48 ? NF48 : NF16) * 64, d);
+            F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
+        } else if constexpr (LPF == 1) {
             uint32_t d[4][4];
             load_chunks<1, 4, NT>(a, koff, act ? klen : 0u, act, rl, d);
             F = fields_small<MODE, SV == 4>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
@@ -1232,7 +1253,8 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
     // the ring alone.  3 workgroups per CU (LDS and, at ~145 VGPRs, registers).
     constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : MODE == 8 ? 2 * RS16 : 1;
     constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE);
-    static_assert(MODE == 0 || RS * kSlot * 16 >= 4096 + kSlot * 16, "ring too small for the scratch");
+    static_assert(MODE == 0 || (RS * kSlot * 16 >= 4096 + kSlot * 16 && RS * kSlot * 16 >= NF * 256 + 4096),
+                  "ring too small for the scratch");
     __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kSlot];
     __shared__ uint32_t s_recf[4][RS];
     __shared__ __attribute__((aligned(16))) uint4 s_pb[DEFER ? 4 : 1][kSlotsPerBucket][DEFER ? 64 : 1];
@@ -1311,8 +1333,10 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
         // wait for them (an s_waitcnt vmcnt(0) per slice in the ISA).
         uint32_t y_off = 0u, y_len = 0u;
         if constexpr (DTOP) load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
-        uint32_t *sf = MODE == 0 ? nullptr : ring.scratch(a, lane, NF * 256, bc);
-        if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : 0>(a, cls, off, len, lane, sf);
+        // parked fields, and the 4 KiB class-0 transpose after them when the slice has any
+        uint32_t *sf = MODE == 0 ? nullptr
+                                 : ring.scratch(a, lane, !(STRIP & 2048) && __ballot(cls == 0) ? NF * 256 + 4096 : NF * 256, bc);
+        if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0>(a, cls, off, len, lane, sf);
@@ -1560,6 +1584,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             break;
         case 41: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true>), dim3(blocks), dim3(256), 0, st, a); break;
         case 33: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, false>), dim3(blocks), dim3(256), 0, st, a); break;
+        // 26: class 0 loaded per lane (each lane its own frame's four chunks), the round-1 form
+        case 26: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 2048>), dim3(blocks), dim3(256), 0, st, a); break;
         // 4 waves per SIMD (at most 128 VGPRs) with the 8-slot ring (4 workgroups per CU fit in LDS)
         case 34: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
@@ -1586,6 +1612,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 34 && a.nbursts == 1) {
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 26 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 2048>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 33 && a.nbursts == 1) {
