@@ -842,16 +842,81 @@ __device__ __forceinline__ bool fc_hit(const FlowCache &fc, const Fields &F)
     return (fc.meta & kFcValid) && fc.ports == F.ports && fc.dst == F.dst && fc.src == bswap32(F.src);
 }
 
-// Classify lane's frame and leave its record in pr.
+__device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int lane, uint32_t *sf,
+                                                      uint32_t (&d)[4][4]);
+
+__device__ __forceinline__ uint32_t probe_bucket(const RxArgs &a, const Fields &F)
+{
+    return tuple_hash(F.ports, F.dst, bswap32(F.src)) & a.t.bucket_mask;
+}
+
+// The first buckets of the wave's 64 probes loaded four lanes to a bucket (lane l: slot l&3
+// of frame 16j + l/4's bucket, 16 whole 64-byte buckets per instruction) and transposed
+// through 4 KiB of LDS, as the small-frame path loads frames.  Each lane loading its own
+// bucket's four slots touched up to 64 lines per instruction: C4 75.3 -> 74.0 us
+// (DESIGN.md §5).  Issue and transpose are separate so the small-frame path can issue the
+// next slice's frames in between (the transpose waits for these loads only).
+struct ProbeLoads {
+    uint4 v0, v1, v2, v3;  // slot lane&3 of the buckets of frames lane/4 + 0, 16, 32, 48
+    uint32_t hb;           // this lane's frame's first bucket
+};
+
+__device__ __forceinline__ ProbeLoads probe_issue_coalesced(const RxArgs &a, const Fields &F, int lane)
+{
+    static_assert(kSlotsPerBucket == 4, "one bucket = four 16-byte slots = four lanes");
+    ProbeLoads L;
+    L.hb = probe_bucket(a, F);
+    const uint4 *bk = a.t.buckets + (lane & 3);
+    const uint32_t h0 = lane_read(L.hb, (lane >> 2)), h1 = lane_read(L.hb, 16 + (lane >> 2));
+    const uint32_t h2 = lane_read(L.hb, 32 + (lane >> 2)), h3 = lane_read(L.hb, 48 + (lane >> 2));
+    L.v0 = bk[(size_t)h0 * kSlotsPerBucket];
+    L.v1 = bk[(size_t)h1 * kSlotsPerBucket];
+    L.v2 = bk[(size_t)h2 * kSlotsPerBucket];
+    L.v3 = bk[(size_t)h3 * kSlotsPerBucket];
+    return L;
+}
+
+// [bucket][slot ^ ((bucket >> 2) & 3)] as transpose_small_slice; lane i gets its own bucket
+__device__ __forceinline__ Probe probe_transpose(const ProbeLoads &L, int lane, uint32_t *tsf)
+{
+    uint4 *t = reinterpret_cast<uint4 *>(tsf);
+    const int ch = lane & 3;
+    const int f0 = lane >> 2, f1 = 16 + (lane >> 2), f2 = 32 + (lane >> 2), f3 = 48 + (lane >> 2);
+    t[f0 * 4 + (ch ^ ((f0 >> 2) & 3))] = L.v0;
+    t[f1 * 4 + (ch ^ ((f1 >> 2) & 3))] = L.v1;
+    t[f2 * 4 + (ch ^ ((f2 >> 2) & 3))] = L.v2;
+    t[f3 * 4 + (ch ^ ((f3 >> 2) & 3))] = L.v3;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    Probe P;
+    P.hb = L.hb;
+    const int sw = (lane >> 2) & 3;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) P.s[k] = t[lane * 4 + (k ^ sw)];
+    __builtin_amdgcn_wave_barrier();  // reads done before the LDS is reused
+    return P;
+}
+
+// Classify lane's frame and leave its record in pr.  tsf: 4 KiB of LDS for the probe's
+// transpose.  STRIP 4096 (experiment build): each lane loads its own bucket (round-1 form).
 template <int MODE, int STRIP = 0>
 __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
-                                               const Fields &F, WaveCounters &wc, Rec &pr, FlowCache &fc)
+                                               const Fields &F, WaveCounters &wc, Rec &pr, FlowCache &fc,
+                                               uint32_t *tsf)
 {
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = valid && et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
-    const Probe P = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, valid, F);
-    classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr, fc, cached);
+    if constexpr ((STRIP & 4096) == 0 && (STRIP & 2) == 0) {
+        const int lane = (int)(threadIdx.x & 63);
+        const Probe P = cached ? probe_none() : probe_transpose(probe_issue_coalesced(a, F, lane), lane, tsf);
+        classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr, fc, cached);
+    } else {
+        (void)tsf;
+        const Probe P = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, valid, F);
+        classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr, fc, cached);
+    }
 }
 
 // Deferred phase B (DEFER kernels): the first bucket of each lane's probe is loaded by
@@ -860,10 +925,6 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
-__device__ __forceinline__ uint32_t probe_bucket(const RxArgs &a, const Fields &F)
-{
-    return tuple_hash(F.ports, F.dst, bswap32(F.src)) & a.t.bucket_mask;
-}
 
 __device__ __forceinline__ void probe_issue_lds(const RxArgs &a, const Fields &F, uint4 (*pb)[64])
 {
@@ -1224,11 +1285,15 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
-    const Probe PR = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, true, F);
+    // Per-lane bucket loads here.  Four lanes to a bucket with the transpose through the
+    // frames' LDS (as the class path does) measured 64 B at 64 K flows 28.8 -> 25.9 us, but
+    // the one-flow C2 burst, which never probes, 19.2 -> 20.6 (more registers live across
+    // the prefetch); the C2 configuration is the one the metric names.
+    const Probe PO = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, true, F);
     if (nxt) issue_small_slice<true>(a, n_off, n_len, lane, vb[1 - P]);
     uint32_t y_off, y_len;
     load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
-    classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PR, wc, rec, fc, cached);
+    classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PO, wc, rec, fc, cached);
     bytes += c_len;
     if (!(STRIP & 4)) {
         if (ring.n == RS) ring.template flush<true>(a, lane, bc);
@@ -1335,7 +1400,8 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
         if constexpr (DTOP) load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
         // parked fields, and the 4 KiB class-0 transpose after them when the slice has any
         uint32_t *sf = MODE == 0 ? nullptr
-                                 : ring.scratch(a, lane, !(STRIP & 2048) && __ballot(cls == 0) ? NF * 256 + 4096 : NF * 256, bc);
+                                 : ring.scratch(a, lane, !(STRIP & 4096) || (!(STRIP & 2048) && __ballot(cls == 0))
+                                                             ? NF * 256 + 4096 : NF * 256, bc);
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
@@ -1369,7 +1435,7 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            classify_store<MODE, STRIP>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc, rec, fcache);
+            classify_store<MODE, STRIP>(a, f, valid, len, unpark_fields<MODE>(sf, lane), wc, rec, fcache, sf + NF * 64);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
             if (!(STRIP & 4)) {
                 if (ring.n == RS) ring.flush(a, lane, bc);
@@ -1586,6 +1652,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 33: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, false>), dim3(blocks), dim3(256), 0, st, a); break;
         // 26: class 0 loaded per lane (each lane its own frame's four chunks), the round-1 form
         case 26: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 2048>), dim3(blocks), dim3(256), 0, st, a); break;
+        // 27: each lane loads its own TCB bucket (the round-1 form)
+        case 27: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 4096>), dim3(blocks), dim3(256), 0, st, a); break;
         // 4 waves per SIMD (at most 128 VGPRs) with the 8-slot ring (4 workgroups per CU fit in LDS)
         case 34: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
@@ -1616,6 +1684,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 26 && a.nbursts == 1) {
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 2048>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 27 && a.nbursts == 1) {
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 4096>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 33 && a.nbursts == 1) {
