@@ -621,12 +621,21 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
     if (!rec_kind_ok(rec_kind)) return fail(-EINVAL, "%s: rec_kind %u", who, rec_kind);
     if (k && !bursts) return fail(-EINVAL, "%s: NULL burst table", who);
     bool any = false;
+    // the kernel reads descriptors as u32 / u16, frames in 16-byte chunks, and writes each
+    // slice's records with 8- or 16-byte vector stores
+    const uintptr_t rec_align = rec_kind == RXG_REC8 ? 8u : 16u;
     for (uint32_t j = 0; j < k; ++j) {
-        if (bursts[j].n && (!bursts[j].off64 || !bursts[j].len || !bursts[j].out))
+        if (!bursts[j].n) continue;
+        if (!bursts[j].off64 || !bursts[j].len || !bursts[j].out)
             return fail(-EINVAL, "%s: NULL device pointer in burst %u", who, j);
-        any |= bursts[j].n != 0;
+        if (((uintptr_t)bursts[j].off64 & 3u) || ((uintptr_t)bursts[j].len & 1u) ||
+            ((uintptr_t)bursts[j].out & (rec_align - 1u)))
+            return fail(-EINVAL, "%s: burst %u: off64 needs 4-byte, len 2-byte, out %u-byte alignment", who, j,
+                        (unsigned)rec_align);
+        any = true;
     }
     if (any && !frames) return fail(-EINVAL, "%s: NULL frame pool", who);
+    if (any && ((uintptr_t)frames & 15u)) return fail(-EINVAL, "%s: frame pool not 16-byte aligned", who);
     c->burst_ok = false;
     int rc = set_device(c);
     if (rc) return rc;
@@ -694,6 +703,8 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
     if (!c || !b) return fail(-EINVAL, "rxg_tx_cksum_dev: NULL argument");
     if (b->n && (!b->frames || !b->off64 || !b->len))
         return fail(-EINVAL, "rxg_tx_cksum_dev: NULL device pointer");
+    if (b->n && (((uintptr_t)b->frames & 15u) || ((uintptr_t)b->off64 & 3u) || ((uintptr_t)b->len & 1u)))
+        return fail(-EINVAL, "rxg_tx_cksum_dev: frames need 16-byte, off64 4-byte, len 2-byte alignment");
     int rc = set_device(c);
     if (rc) return rc;
     LaunchBurst one{b->off64, b->len, b->n, nullptr};

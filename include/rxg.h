@@ -298,7 +298,8 @@ int rxg_arp_disable(rxg_ctx *ctx);
    + len[i]); the bytes up to the next 64-byte boundary must be readable
    (their contents are ignored), and so must the first 64 bytes at `frames`
    (loads for chunks outside a frame are redirected there, then discarded).
-   len[i] = rte_pktmbuf_data_len(m). */
+   len[i] = rte_pktmbuf_data_len(m).  Alignment (else -EINVAL): frames 16 bytes, off64 4,
+   len 2, out 8 (RXG_REC8) or 16 bytes. */
 typedef struct rxg_dev_batch {
     const void *frames;     /* dev */
     const uint32_t *off64;  /* dev, n entries, in 64-byte units */
