@@ -70,6 +70,7 @@ struct Cand {
 };
 
 
+template <bool HDR = true>
 __device__ __forceinline__ Cand candidate(const PgArgs &a, uint32_t i)
 {
     Cand c{0ull, 0u, 0u};
@@ -101,7 +102,8 @@ __device__ __forceinline__ Cand candidate(const PgArgs &a, uint32_t i)
     if (verdict > RXG_V_RST_LISTEN_NONSYN || datalen <= 0 || (rflags & RXG_F_TRUNC)) return c;
     const uint64_t base = (uint64_t)off * 64u;
     // bytes 44..47 of the frame (>= 54 bytes: not RXG_F_TRUNC); data_off is byte 46
-    const uint32_t dw = *reinterpret_cast<const uint32_t *>(a.frames + base + 44u);
+    // (HDR false, experiment build only, timing: data_off taken as 5 without the load)
+    const uint32_t dw = HDR ? *reinterpret_cast<const uint32_t *>(a.frames + base + 44u) : 0x00500000u;
     const uint32_t start = RXG_OFF_TCP + ((dw >> 20) & 0xFu) * 4u;
     if (start + (uint32_t)datalen > flen) return c;
     c.src = base + start;
@@ -461,7 +463,7 @@ __device__ __forceinline__ uint32_t look_back(const PgArgs &a, uint32_t vb, int 
 // FPT frames per thread (workgroup = 256 * FPT frames, thread t owns frames FPT*t ..
 // FPT*t + FPT-1 for the scan; wave w copies frames [64 FPT w, 64 FPT (w+1)) 64 at a time).
 // TICKET: virtual workgroup ids from an atomic ticket (dispatch-order independent).
-template <int kU, bool NT, int FPT, bool TICKET, int PRE = 0, int TPB = kPgThreads>
+template <int kU, bool NT, int FPT, bool TICKET, int PRE = 0, int TPB = kPgThreads, bool HDR = true>
 __global__ __launch_bounds__(TPB) void pg_gather(PgArgs a)
 {
     constexpr int FPB = TPB * FPT;
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(TPB) void pg_gather(PgArgs a)
     uint32_t mine = 0;
 #pragma unroll
     for (int k = 0; k < FPT; ++k) {
-        c[k] = candidate(a, i0 + k);
+        c[k] = candidate<HDR>(a, i0 + k);
         mine += (c[k].len + 15u) >> 4;
     }
     const uint32_t incl = wave_incl_scan(mine, lane);
@@ -630,6 +632,8 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     case 10: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 256>), g, b, 0, st, a); break;
     case 11: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 1024>), g, b, 0, st, a); break;
     case 12: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 512>), g, b, 0, st, a); break;
+    // 13: production without the frame header-word load (timing only: data_off taken as 5)
+    case 13: hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd, false>), g, b, 0, st, a); break;
     default: hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
     }
 #else
