@@ -926,13 +926,24 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
 
+// Issued by inline assembly, so the compiler does not know an LDS-DMA is in flight: with the
+// builtin it waits vmcnt(0) at the next use of any load result (the loop's back edge),
+// draining the probe.  The reader waits itself (probe_lds_wait) before reading pb.
 __device__ __forceinline__ void probe_issue_lds(const RxArgs &a, const Fields &F, uint4 (*pb)[64])
 {
     const uint4 *b = a.t.buckets + (size_t)probe_bucket(a, F) * kSlotsPerBucket;
 #pragma unroll
-    for (int k = 0; k < kSlotsPerBucket; ++k)
-        __builtin_amdgcn_global_load_lds((glb_void_t *)(b + k), (lds_void_t *)&pb[k][0], 16, 0, 0);
+    for (int k = 0; k < kSlotsPerBucket; ++k) {
+        const uint32_t lds = (uint32_t)(uintptr_t)(lds_void_t *)&pb[k][0];
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(b + k), "s"(__builtin_amdgcn_readfirstlane(lds))
+                     : "memory");
+    }
 }
+
+__device__ __forceinline__ void probe_lds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ Probe probe_from_lds(const RxArgs &a, const Fields &F, const uint4 (*pb)[64], int lane)
 {
@@ -1349,12 +1360,18 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
     load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
     // DEFER: the slice whose phase B is pending (wave-uniform; ~0 = none), its fields
     uint32_t d_s = ~0u, d_len = 0u;
+    bool d_issue = false;  // the pending slice's probe DMA is still to be issued
     bool d_cached = true;
     Fields dF{};
     auto finish_pending = [&]() {
         if constexpr (DEFER) {
             if (d_s == ~0u) return;
             const bool dvalid = (uint32_t)lane < slice_frames(a, uniform(d_s), bc);
+            if (d_issue) {  // not issued yet (a small-slice run or the end follows): now
+                probe_issue_lds(a, dF, s_pb[wid]);
+                d_issue = false;
+            }
+            if (!d_cached) probe_lds_wait();
             const Probe P = d_cached ? probe_none() : probe_from_lds(a, dF, s_pb[wid], lane);
             classify_finish<MODE, STRIP>(a, d_s * 64u + (uint32_t)lane, dvalid, d_len, dF, P, wc, rec, fcache,
                                          d_cached);
@@ -1398,6 +1415,12 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
         // wait for them (an s_waitcnt vmcnt(0) per slice in the ISA).
         uint32_t y_off = 0u, y_len = 0u;
         if constexpr (DTOP) load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
+        if constexpr (DEFER) {
+            if (d_issue) {
+                probe_issue_lds(a, dF, s_pb[wid]);
+                d_issue = false;
+            }
+        }
         // parked fields, and the 4 KiB class-0 transpose after them when the slice has any
         uint32_t *sf = MODE == 0 ? nullptr
                                  : ring.scratch(a, lane, !(STRIP & 4096) || (!(STRIP & 2048) && __ballot(cls == 0))
@@ -1425,7 +1448,13 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
             const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
             const bool is_tcp = valid && et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
             d_cached = __ballot(is_tcp && !fc_hit(fcache, F)) == 0ull;
-            if (!d_cached) probe_issue_lds(a, F, s_pb[wid]);
+            // every register the loop's back edge copies has been waited for before the
+            // LDS-DMA is issued: with an LDS-DMA in flight the compiler waits vmcnt(0) at the
+            // next use of any load result, which would drain the probe at the back edge
+            // the probe's DMA is issued at the next class-path slice's start, after the loop's
+            // back edge (whose register copies wait for their loads: a DMA in flight there
+            // would be drained with them)
+            d_issue = !d_cached;
             d_s = s;
             d_len = len;
             dF = F;

@@ -23,6 +23,8 @@ WL = {"c3": (1500, 1000, 0, 2), "c3r1": (1500, 1000, 0, 1), "c4r4": (0, 65536, 1
       "c2r1": (64, 1, 0, 1), "c2x4": (64, 1, 0, 4),
       # single-size legs of the IMIX (64 K flows): where C4's time goes
       "u64": (64, 65536, 0, 16), "u576": (576, 65536, 0, 2), "u1500": (1500, 65536, 0, 1),
+      # C4's IMIX at other flow counts (the TCB table's size: 16 K flows 1 MiB ... 256 K 16 MiB)
+      "c4f1k": (0, 1024, 1, 3), "c4f16k": (0, 16384, 1, 3), "c4f256k": (0, 262144, 1, 3),
       # C2 as 16 bursts of one 1 GiB pool per launch (rxg_rx_bursts_dev, bench.py multiburst_leg)
       "c2m": (64, 1, 0, 1)}
 MULTI = 16
