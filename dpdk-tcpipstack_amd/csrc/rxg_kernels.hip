@@ -749,7 +749,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
         int rl = lane;
         asm volatile("" : "+v"(rl));  // keep per-round lane math inside the round (VGPRs)
         Fields F;
-        if constexpr (LPF == 1 && MODE != 0 && SV != 6) {
+        if constexpr (LPF == 1 && SV != 6 && SV != 4) {
             // The class's frames are loaded as the all-small path loads a slice (lane l:
             // chunk l&3 of frame 16j + l/4, 16 whole frames and 16 lines per instruction) and
             // transposed through LDS (4 KiB after the parked fields).  Lane i loading its own
@@ -765,7 +765,8 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
                 v[j] = load16<NT>(ok ? a.frames + (size_t)foff * 64u + ch * 16 : a.frames);
             }
             uint32_t d[4][4];
-            transpose_small_slice(v, rl, sf + (MODE == 48 ? NF48 : NF16) * 64, d);
+            // (MODE 0, tx: no parked fields; the transpose uses the 4 KiB ring area itself)
+            transpose_small_slice(v, rl, sf + (MODE == 0 ? 0 : MODE == 48 ? NF48 * 64 : NF16 * 64), d);
             F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
         } else if constexpr (LPF == 1) {
             uint32_t d[4][4];
@@ -1327,7 +1328,8 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
     // REC48: 4 of 3 KiB); its free slots are also the scratch of the slice in
     // progress (4 KiB small-slice transpose, NF x 256 B parked fields), so LDS per wave is
     // the ring alone.  3 workgroups per CU (LDS and, at ~145 VGPRs, registers).
-    constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : MODE == 8 ? 2 * RS16 : 1;
+    // (tx, MODE 0: 4 x 1 KiB, the class-0 transpose's scratch; no records)
+    constexpr int RS = MODE == 16 ? RS16 : MODE == 48 ? 4 : MODE == 8 ? 2 * RS16 : 4;
     constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE);
     static_assert(MODE == 0 || (RS * kSlot * 16 >= 4096 + kSlot * 16 && RS * kSlot * 16 >= NF * 256 + 4096),
                   "ring too small for the scratch");
@@ -1422,7 +1424,7 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
             }
         }
         // parked fields, and the 4 KiB class-0 transpose after them when the slice has any
-        uint32_t *sf = MODE == 0 ? nullptr
+        uint32_t *sf = MODE == 0 ? reinterpret_cast<uint32_t *>(ring.img[0])
                                  : ring.scratch(a, lane, !(STRIP & 4096) || (!(STRIP & 2048) && __ballot(cls == 0))
                                                              ? NF * 256 + 4096 : NF * 256, bc);
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
@@ -1746,6 +1748,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 64>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 21)  // header lines stored to a contiguous array (C3 frames only)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 128>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 28)  // class 0 loaded per lane (before the transpose)
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 2048>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 24)  // 64-byte frames rewritten as a whole line
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 512>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 25)  // longer frames: only the two 16-byte chunks with the fields
