@@ -13,6 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -57,6 +60,75 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// Host threads that pack large host bursts into the pinned staging (rxg_rx_burst), started
+// at the first burst that needs them and kept for the context's life: no thread is
+// created per burst.
+class PackPool {
+  public:
+    ~PackPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    // Runs fn(0) .. fn(n - 1), fn(0) on the calling thread; returns when all are done.
+    void run(uint32_t n, const std::function<void(uint32_t)> &fn)
+    {
+        if (n <= 1) {
+            fn(0);
+            return;
+        }
+        while (th_.size() < n - 1) {
+            const uint32_t id = (uint32_t)th_.size() + 1;
+            th_.emplace_back([this, id] { worker(id); });
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &fn;
+            n_ = n;
+            pending_ = n - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void worker(uint32_t id)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(uint32_t)> *job;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (id >= n_) continue;  // not needed for this burst
+                job = job_;
+            }
+            (*job)(id);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint32_t)> *job_ = nullptr;
+    uint32_t n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 struct rxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -65,6 +137,7 @@ struct rxg_ctx {
     // Experiment switches: only an experiment build (make experiments, -DRXG_EXPERIMENTS,
     // rxg/librxg_exp.so for scripts/kbench.py and pgbench.py) reads them from the
     // environment; in the product library they stay 0.
+    PackPool pack_pool;  // rxg_rx_burst's packing threads
     int variant = 0;     // RXG_VARIANT: rx kernel variants (class subsets, ablations)
     int nocount = 0;     // RXG_NOCOUNT: skip the counter reduction
     int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather variants
@@ -759,15 +832,9 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
                             (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off, pkts[i].data_len);
     };
     const uint32_t nthr = (uint32_t)std::min<uint64_t>(8u, std::max<uint64_t>(1u, (slot * 64u) >> 22));
-    if (nthr <= 1) {
-        pack(0, n);
-    } else {
-        std::vector<std::thread> th;
-        for (uint32_t t = 1; t < nthr; ++t)
-            th.emplace_back(pack, (uint32_t)((uint64_t)n * t / nthr), (uint32_t)((uint64_t)n * (t + 1) / nthr));
-        pack(0, (uint32_t)((uint64_t)n / nthr));
-        for (auto &x : th) x.join();
-    }
+    c->pack_pool.run(nthr, [&](uint32_t t) {
+        pack((uint32_t)((uint64_t)n * t / nthr), (uint32_t)((uint64_t)n * (t + 1) / nthr));
+    });
     if (n == 0) {  // still a burst: posted writes drained, replay state reset
         rxg_dev_batch e{};
         e.rec_kind = rec_kind;

@@ -176,6 +176,22 @@ def test_host_burst_matches_device_burst(engine):
     assert_records_equal(a, exp, frames)
 
 
+def test_large_host_bursts_use_the_packing_pool(engine):
+    """Host bursts over 4 MiB are packed by several threads (rxg_rx_burst's pool, kept for
+    the context's life): two such bursts in a row, records equal to the device path's."""
+    rng = np.random.default_rng(43)
+    rows = [(80, 0, pktgen.raw_of_host(pktgen.ip4(192, 168, 78, 2)), 0, 1)]
+    tcb, live = pktgen.table_arrays(rows)
+    engine.tcb_load(tcb, live)
+    for k in range(2):
+        frames = [pktgen.frame(sport=1000 + i % 5000, payload=rng.bytes(int(rng.integers(0, 1400))))
+                  for i in range(24000)]
+        got = engine.rx_burst(frames, rxg.REC8)
+        arena, off, lens = pktgen.pack_arena(frames)
+        assert arena.size > (12 << 20)  # at least three packing threads
+        assert got.tobytes() == engine.rx_arena(arena, off, lens, rxg.REC8).tobytes()
+
+
 def test_tx_generate_golden(engine):
     g = np.load(os.path.join(GOLD, "rx_golden.npz"))
     t = np.load(os.path.join(GOLD, "tx_golden.npz"))
