@@ -562,22 +562,17 @@ __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32
     return F;
 }
 
-template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV = 0>
-__device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off, uint32_t len, bool active,
-                                                   int lane)
+// The loads of one round of a streaming class: lane l of a group of LPF loads chunks
+// l, l + LPF, ... of its frame.  Inactive lanes: off = len = 0 (the arena's first SAFE bytes
+// exist: it holds a frame of this class).
+template <int C, int LPF, int NLOAD, bool NT>
+__device__ __forceinline__ void round_load(const RxArgs &a, uint32_t off, uint32_t len, int lane,
+                                           uint32_t (&d)[NLOAD][4])
 {
-    static_assert(LPF >= 2 && LPF <= 64, "streaming classes only");
-    constexpr bool TX = MODE == 0;
     constexpr int SAFE = (class_min_len(C) + 63) & ~63;  // bytes every frame of the class has
     const int gl = lane & (LPF - 1);
-    const int gbase = lane - gl;
-    const bool leader = active && gl == 0;
-    // inactive lanes: off = len = 0 (the arena's first SAFE bytes exist: it holds a frame of
-    // this class)
-    uint8_t *fp = const_cast<uint8_t *>(a.frames) + (size_t)off * 64u;
+    const uint8_t *fp = a.frames + (size_t)off * 64u;
     const uint32_t lastc = len ? ((len - 1u) & ~15u) : 0u;
-
-    uint32_t d[NLOAD][4];
 #pragma unroll
     for (int j = 0; j < NLOAD; ++j) {
         const uint32_t o = (uint32_t)(gl + j * LPF) * 16u;
@@ -588,6 +583,32 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
             v = load16<NT>(fp + min(o, lastc));
         d[j][0] = v.x; d[j][1] = v.y; d[j][2] = v.z; d[j][3] = v.w;
     }
+}
+
+template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV = 0>
+__device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                                      int lane, uint32_t (&d)[NLOAD][4]);
+
+template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV = 0>
+__device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                                   int lane)
+{
+    uint32_t d[NLOAD][4];
+    round_load<C, LPF, NLOAD, NT>(a, off, len, lane, d);
+    return frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, off, len, active, lane, d);
+}
+
+// Sums, header fields and (tx) checksum stores of one round whose chunks are in d.
+template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV>
+__device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
+                                                      int lane, uint32_t (&d)[NLOAD][4])
+{
+    static_assert(LPF >= 2 && LPF <= 64, "streaming classes only");
+    constexpr bool TX = MODE == 0;
+    const int gl = lane & (LPF - 1);
+    const int gbase = lane - gl;
+    const bool leader = active && gl == 0;
+    uint8_t *fp = const_cast<uint8_t *>(a.frames) + (size_t)off * 64u;
 
     // ---- TCP span bytes from 32 on (chunk >= 2), masked at data_len.  Bytes [26, 32) come
     // from the leader's header dwords below.
@@ -711,7 +732,7 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
 __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int lane, uint32_t *sf,
                                                       uint32_t (&d)[4][4]);
 
-template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int SV = 0>
+template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int SV = 0, bool PIPE = false>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
                                           int lane_in, uint32_t *sf)
 {
@@ -733,6 +754,52 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
         corig = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), lane);
         coff = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)off);
         clen = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)len);
+    }
+    if constexpr (PIPE && LPF >= 2 && !JUMBO) {
+        // Rounds software-pipelined: round r + 1's loads are issued before round r is
+        // waited for, into the other of two register buffers (the steps alternate, so no
+        // register copy of a load in flight).  The issue is unconditional (a round past the
+        // class's last frame loads the arena's first bytes, all lanes inactive): a load
+        // under a branch would leave the wait at the join counting as if it were absent.
+        uint32_t dA[NLOAD][4], dB[NLOAD][4];
+        auto rmeta = [&](uint32_t r, uint32_t &korig, uint32_t &koff, uint32_t &klen) -> bool {
+            int rl = lane;
+            asm volatile("" : "+v"(rl));
+            const uint32_t k = r + (uint32_t)(rl / LPF);
+            const int src = (int)(k & 63u);
+            korig = lane_read(corig, src);
+            koff = lane_read(coff, src);
+            klen = lane_read(clen, src);
+            const bool act = k < cnt;
+            if (!act) koff = klen = 0u;
+            return act;
+        };
+        uint32_t ao, aoff, alen, bo, boff, blen;
+        bool aact = rmeta(0u, ao, aoff, alen), bact;
+        round_load<C, LPF, NLOAD, NT>(a, aoff, alen, lane, dA);
+        for (uint32_t r = 0;;) {
+            bact = rmeta(r + FPW, bo, boff, blen);
+            round_load<C, LPF, NLOAD, NT>(a, boff, blen, lane, dB);
+            {
+                const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, aoff, alen, aact, lane, dA);
+                if constexpr (MODE != 0) {
+                    if (aact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, ao, F);
+                }
+            }
+            r += FPW;
+            if (r >= cnt) break;
+            aact = rmeta(r + FPW, ao, aoff, alen);
+            round_load<C, LPF, NLOAD, NT>(a, aoff, alen, lane, dA);
+            {
+                const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, boff, blen, bact, lane, dB);
+                if constexpr (MODE != 0) {
+                    if (bact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, bo, F);
+                }
+            }
+            r += FPW;
+            if (r >= cnt) break;
+        }
+        return;
     }
     for (uint32_t r = 0; r < cnt; r += FPW) {
         const uint32_t k = r + (uint32_t)(lane / LPF);
@@ -1318,8 +1385,10 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
 }
 
 template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
-          bool DEFER = false, bool DTOP = true, int WPE = 1>
-__global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
+          bool DEFER = false, bool DTOP = true, int WPE = 0>
+// WPE 0: 3 waves per SIMD (at most 168 VGPRs) for the software-pipelined rounds, which
+// would otherwise take 170 and drop to 2; no bound for the forms without them
+__global__ __launch_bounds__(256, WPE ? WPE : (((STRIP & 8192) || MULTI || DEFER || MODE == 48) ? 1 : 3)) void rx_kernel(RxArgs a)
 {
     static_assert(!DEFER || MODE == 8 || MODE == 16, "deferred phase B: REC8 / REC16 only");
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -1427,15 +1496,21 @@ __global__ __launch_bounds__(256, WPE) void rx_kernel(RxArgs a)
         uint32_t *sf = MODE == 0 ? reinterpret_cast<uint32_t *>(ring.img[0])
                                  : ring.scratch(a, lane, !(STRIP & 4096) || (!(STRIP & 2048) && __ballot(cls == 0))
                                                              ? NF * 256 + 4096 : NF * 256, bc);
+        constexpr int SVS = (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0;
+        // The streaming classes' rounds software-pipelined; STRIP 8192
+        // (experiment) = the round-2 form.  Multi-burst kernels keep that form: with the burst
+        // table held in lanes the pipelined rounds need 176 VGPRs (2 waves per SIMD); so do
+        // 48-byte records (168 with 16 B/lane spilled).
+        constexpr bool PIPE = !(STRIP & 8192) && !MULTI && !DEFER && MODE != 48;
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false, 0, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false, 0, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 7) & 1) run_class<7, 64, 2, true, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr (MODE == 0 || (STRIP & 8)) {
             wcount(wc, RXG_C_RX, valid);
@@ -1685,6 +1760,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 26: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 2048>), dim3(blocks), dim3(256), 0, st, a); break;
         // 27: each lane loads its own TCB bucket (the round-1 form)
         case 27: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 4096>), dim3(blocks), dim3(256), 0, st, a); break;
+        // 42: streaming-class rounds not pipelined (the round-2 form)
+        case 42: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 8192>), dim3(blocks), dim3(256), 0, st, a); break;
         // 4 waves per SIMD (at most 128 VGPRs) with the 8-slot ring (4 workgroups per CU fit in LDS)
         case 34: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
@@ -1707,6 +1784,14 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 41 && a.nbursts == 1) {
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, false, true>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 42 && a.nbursts == 1) {  // streaming-class rounds not pipelined (round 2)
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 8192>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 43 && a.nbursts == 1) {  // pipelined at its natural 170 VGPRs, 2 waves per SIMD
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, true, 1>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 34 && a.nbursts == 1) {
@@ -1748,6 +1833,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 64>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 21)  // header lines stored to a contiguous array (C3 frames only)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 128>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 42)  // streaming-class rounds not pipelined (round 2)
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 8192>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 28)  // class 0 loaded per lane (before the transpose)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 2048>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 24)  // 64-byte frames rewritten as a whole line

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--frames-c2", type=int, default=0, help="override frames for c2* workloads")
     ap.add_argument("--rec", type=int, default=16)
     ap.add_argument("--tx", action="store_true", help="time rxg_tx_cksum_dev (rx_kernel<0>) instead")
+    ap.add_argument("--check", action="store_true",
+                    help="also compare every variant's records (and counters) with the first variant's")
     args = ap.parse_args()
 
     base = rxg.Engine(0)
@@ -111,6 +113,29 @@ def main():
                     libs[v].rxg_event_destroy(eng.ctx, a)
                     libs[v].rxg_event_destroy(eng.ctx, b)
                 rxg._lib = main_lib
+    if args.check and not args.tx:
+        for w, (bs, nbytes, tcb, live, nfr) in wls.items():
+            ref = None
+            for v, eng in engines.items():
+                rxg._lib = libs[v]
+                eng.tcb_load(tcb, live)
+                eng.tcb_sync()
+                eng.counters_reset()
+                if w == "c2m":
+                    b = bs[0]
+                    eng.rx_bursts_dev(b["arena"].ptr, [(b["off64"].ptr + j * nfr * 4, b["len"].ptr + j * nfr * 2,
+                                                        nfr, out.ptr + j * nfr * args.rec) for j in range(MULTI)], args.rec)
+                    nrec = nfr * MULTI
+                else:
+                    eng.rx_burst_dev(bs[0]["arena"].ptr, bs[0]["off64"].ptr, bs[0]["len"].ptr, nfr, out.ptr, args.rec)
+                    nrec = nfr
+                eng.sync()
+                got = (out.download(np.uint8, nrec * args.rec).tobytes(), tuple(eng.counters()))
+                rxg._lib = main_lib
+                if ref is None:
+                    ref = got
+                print(json.dumps({"check": w, "variant": v, "records_equal": got[0] == ref[0],
+                                  "counters_equal": got[1] == ref[1]}), flush=True)
     for (v, w), ms in res.items():
         nbytes = wls[w][1]
         med = float(np.median(ms))
