@@ -755,12 +755,12 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
         coff = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)off);
         clen = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)len);
     }
+    // Rounds software-pipelined: round r + 1's loads are issued before round r is waited
+    // for, into the other of two register buffers (the steps alternate, so no register copy
+    // of a load in flight).  Loads are issued unconditionally, a round past the class's last
+    // frame reading the arena's first bytes with every lane inactive: a load under a branch
+    // leaves the wait at the join counting as if it were absent (vmcnt(0)).  DESIGN.md §5.
     if constexpr (PIPE && LPF >= 2 && !JUMBO) {
-        // Rounds software-pipelined: round r + 1's loads are issued before round r is
-        // waited for, into the other of two register buffers (the steps alternate, so no
-        // register copy of a load in flight).  The issue is unconditional (a round past the
-        // class's last frame loads the arena's first bytes, all lanes inactive): a load
-        // under a branch would leave the wait at the join counting as if it were absent.
         uint32_t dA[NLOAD][4], dB[NLOAD][4];
         auto rmeta = [&](uint32_t r, uint32_t &korig, uint32_t &koff, uint32_t &klen) -> bool {
             int rl = lane;
@@ -775,10 +775,13 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             return act;
         };
         uint32_t ao, aoff, alen, bo, boff, blen;
-        bool aact = rmeta(0u, ao, aoff, alen), bact;
+        bool aact = rmeta(0u, ao, aoff, alen);
         round_load<C, LPF, NLOAD, NT>(a, aoff, alen, lane, dA);
-        for (uint32_t r = 0;;) {
-            bact = rmeta(r + FPW, bo, boff, blen);
+        // one loop body, no exit in its middle: the loads of both buffers are issued every
+        // iteration and only round B's compute is conditional, so the wait for each buffer
+        // counts exactly the other buffer's loads issued after it
+        for (uint32_t r = 0; r < cnt; r += 2u * FPW) {
+            const bool bact = rmeta(r + FPW, bo, boff, blen);
             round_load<C, LPF, NLOAD, NT>(a, boff, blen, lane, dB);
             {
                 const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, aoff, alen, aact, lane, dA);
@@ -786,18 +789,14 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
                     if (aact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, ao, F);
                 }
             }
-            r += FPW;
-            if (r >= cnt) break;
-            aact = rmeta(r + FPW, ao, aoff, alen);
+            aact = rmeta(r + 2u * FPW, ao, aoff, alen);
             round_load<C, LPF, NLOAD, NT>(a, aoff, alen, lane, dA);
-            {
+            if (r + FPW < cnt) {
                 const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, boff, blen, bact, lane, dB);
                 if constexpr (MODE != 0) {
                     if (bact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, bo, F);
                 }
             }
-            r += FPW;
-            if (r >= cnt) break;
         }
         return;
     }

@@ -2,7 +2,7 @@
 # Pipelined streaming-class rounds as production: GPU tests, A/B against the round-2 form
 # (experiment variant 42), bench line.
 set -u
-O=gpurun_out/pipe2; mkdir -p $O
+O=gpurun_out/${TAG:-pipe2}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; echo STOP tests; exit 1; }
 tail -2 $O/pytest_gpu.log
