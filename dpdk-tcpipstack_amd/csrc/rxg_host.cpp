@@ -403,6 +403,36 @@ extern "C" int rxg_tcb_load(rxg_ctx *c, const rxg_tcb_tuple *tcbs, const uint8_t
 
 extern "C" int32_t rxg_tcb_count(rxg_ctx *c) { return c ? c->mir.ntcb() : -EINVAL; }
 
+extern "C" int rxg_flow_partition(rxg_ctx *c, uint32_t part, uint32_t nparts)
+{
+    if (!c) return fail(-EINVAL, "rxg_flow_partition: ctx NULL");
+    if (nparts == 0 || nparts > RXG_RSS_RETA_SIZE || part >= nparts)
+        return fail(-EINVAL, "rxg_flow_partition: part %u of %u", part, nparts);
+    if (c->mir.part == part && c->mir.nparts == nparts) return 0;
+    c->mir.part = part;
+    c->mir.nparts = nparts;
+    c->mir.need_rebuild = true;  // the whole table, as after rxg_tcb_load
+    c->dirty = true;
+    c->touched_all = true;
+    c->gen++;
+    return 0;
+}
+
+extern "C" uint32_t rxg_rss_hash(const uint8_t tuple12[12]) { return tuple12 ? rss_toeplitz(tuple12, 12) : 0u; }
+
+extern "C" int rxg_flow_part_of(const uint8_t *f, uint32_t len, uint32_t nparts)
+{
+    if ((!f && len) || nparts == 0) return fail(-EINVAL, "rxg_flow_part_of: frame NULL or nparts 0");
+    uint8_t b[38] = {0};
+    std::memcpy(b, f, std::min<uint32_t>(len, 38u));
+    // ether_in's demux and ip_in's protocol test (etherin.c:12-37, ip.c:19-42): only TCP
+    // over IPv4 reaches findtcb
+    if (b[12] != 0x08 || b[13] != 0x00 || b[23] != RXG_IPPROTO_TCP) return 0;
+    return (int)rss_queue(rss_toeplitz(b + 26, 12), nparts);
+}
+
+extern "C" int64_t rxg_tcb_keys(rxg_ctx *c) { return c ? (int64_t)c->mir.nkeys() : -EINVAL; }
+
 extern "C" int rxg_tcb_post(rxg_ctx *c, const rxg_tcb_op *op)
 {
     if (!c || !op) return fail(-EINVAL, "rxg_tcb_post: NULL argument");

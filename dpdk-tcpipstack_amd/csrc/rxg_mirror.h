@@ -73,8 +73,43 @@ inline bool tcb_key(const rxg_tcb_tuple &t, TupleKey &k)
     return true;
 }
 
+// ---- flow-affinity sharding: the Toeplitz RSS hash NICs steer rx queues by
+// (Microsoft RSS, the 40-byte key DPDK drivers default to), over the 12 wire bytes IPv4/TCP
+// hashes: src ip | dst ip | src port | dst port = frame bytes 26..37, and the default
+// redirection table (RXG_RSS_RETA_SIZE entries filled round-robin: entry i -> queue i % n).
+static const uint8_t kRssKey[40] = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+                                    0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+                                    0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+inline uint32_t rss_toeplitz(const uint8_t *in, int n)
+{
+    uint32_t h = 0, win = ((uint32_t)kRssKey[0] << 24) | ((uint32_t)kRssKey[1] << 16) | ((uint32_t)kRssKey[2] << 8) | kRssKey[3];
+    for (int i = 0; i < n; ++i) {
+        const uint8_t nk = kRssKey[i + 4];
+        for (int b = 7; b >= 0; --b) {
+            if ((in[i] >> b) & 1) h ^= win;
+            win = (win << 1) | ((nk >> b) & 1u);
+        }
+    }
+    return h;
+}
+inline uint32_t rss_queue(uint32_t h, uint32_t nparts) { return (h % RXG_RSS_RETA_SIZE) % nparts; }
+// A pass-1 key's wire bytes: src ip is held in host order (ntohl), dst raw as read, ports
+// as (dport << 16) | sport in host order (tcp_tcb.c:152-155)
+inline uint32_t key_part(const TupleKey &k, uint32_t nparts)
+{
+    const uint8_t w[12] = {(uint8_t)(k.src >> 24), (uint8_t)(k.src >> 16), (uint8_t)(k.src >> 8), (uint8_t)k.src,
+                           (uint8_t)k.dst, (uint8_t)(k.dst >> 8), (uint8_t)(k.dst >> 16), (uint8_t)(k.dst >> 24),
+                           (uint8_t)(k.ports >> 8), (uint8_t)k.ports, (uint8_t)(k.ports >> 24), (uint8_t)(k.ports >> 16)};
+    return rss_queue(rss_toeplitz(w, 12), nparts);
+}
+
 class TcbMirror {
   public:
+    // Flow-affinity partition: with nparts > 1 the exact-tuple table holds only the keys whose
+    // RSS queue is `part`; the listener map, liveness and the lowest NULL slot stay whole
+    // (findtcb's pass 2 reads the whole slot array), so a frame steered here classifies as
+    // against the whole table.
+    uint32_t part = 0, nparts = 1;
     // canonical host copy of tcbs[0..Ntcb)
     std::vector<rxg_tcb_tuple> tcb;
     std::vector<uint8_t> live;
@@ -237,7 +272,10 @@ class TcbMirror {
     static constexpr uint32_t kNone = 0xFFFFFFFFu;
     std::vector<uint32_t> slot_pp, listen_pp;  // word -> its pending patch, or kNone
 
-    static bool key_of(const rxg_tcb_tuple &t, TupleKey &k) { return tcb_key(t, k); }
+    bool key_of(const rxg_tcb_tuple &t, TupleKey &k) const
+    {
+        return tcb_key(t, k) && (nparts <= 1 || key_part(k, nparts) == part);
+    }
     static bool same_key(const rxg_tcb_tuple &a, const rxg_tcb_tuple &b)
     {
         return a.dport == b.dport && a.sport == b.sport && a.ipv4_dst == b.ipv4_dst && a.ipv4_src == b.ipv4_src;

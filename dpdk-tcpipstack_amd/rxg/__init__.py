@@ -97,6 +97,7 @@ class RxgError(RuntimeError):
 
 # ------------------------------------------------------------------- ctypes structs ---
 ABI_VERSION = 2
+RSS_RETA_SIZE = 128  # rxg.h RXG_RSS_RETA_SIZE: the default redirection table
 
 
 class Config(C.Structure):
@@ -213,6 +214,10 @@ def load_library(path: str = LIB_PATH):
         "rxg_tcb_load": (C.c_int, [vp, vp, vp, i32]),
         "rxg_tcb_sync": (C.c_int, [vp]),
         "rxg_tcb_count": (i32, [vp]),
+        "rxg_flow_partition": (C.c_int, [vp, u32, u32]),
+        "rxg_flow_part_of": (C.c_int, [C.c_char_p, u32, u32]),
+        "rxg_rss_hash": (u32, [C.c_char_p]),
+        "rxg_tcb_keys": (C.c_int64, [vp]),
         "rxg_tcb_post": (C.c_int, [vp, C.POINTER(TcbOp)]),
         "rxg_tcb_drain": (C.c_int, [vp]),
         "rxg_arp_load": (C.c_int, [vp, vp, u32]),
@@ -390,6 +395,20 @@ class PinnedArray:
             self.ptr = None
 
 
+def flow_part_of(frame: bytes, nparts: int) -> int:
+    """The RSS queue (0 .. nparts-1) whose context classifies this frame (rxg_flow_part_of)."""
+    r = load_library().rxg_flow_part_of(frame, len(frame), nparts)
+    if r < 0:
+        raise RxgError(f"rxg_flow_part_of failed ({r})")
+    return r
+
+
+def rss_hash(tuple12: bytes) -> int:
+    """Toeplitz RSS hash (default Microsoft key) of src ip | dst ip | src port | dst port."""
+    assert len(tuple12) == 12
+    return load_library().rxg_rss_hash(tuple12)
+
+
 class Engine:
     """One rxg context on one GPU (include/rxg.h: rxg_init .. rxg_fini)."""
 
@@ -483,6 +502,13 @@ class Engine:
 
     def tcb_count(self) -> int:
         return _lib.rxg_tcb_count(self.ctx)
+
+    # --- flow-affinity sharding (rxg_flow_partition): this context serves RSS queue `part`
+    def flow_partition(self, part: int, nparts: int):
+        _check(_lib.rxg_flow_partition(self.ctx, part, nparts), "rxg_flow_partition")
+
+    def tcb_keys(self) -> int:
+        return _lib.rxg_tcb_keys(self.ctx)
 
     # --- writes from other threads (rxg_tcb_post: lock-free, applied at the next burst)
     def tcb_post_upsert(self, idx: int, dport: int, sport: int, ipv4_dst: int, ipv4_src: int,

@@ -255,6 +255,27 @@ int rxg_tcb_sync(rxg_ctx *ctx);
 /* Current Ntcb of the mirror. */
 int32_t rxg_tcb_count(rxg_ctx *ctx);
 
+/* Flow-affinity sharding (SURVEY.md §8(e)'s optional mode): one rx queue per
+   GPU, the NIC steering each TCP segment to a queue by its RSS hash (Toeplitz over src ip,
+   dst ip, src port, dst port with the default 40-byte Microsoft key, then a redirection table
+   of RXG_RSS_RETA_SIZE entries filled round-robin, DPDK's default).  The context of queue
+   `part` of `nparts` keeps in its device table only the tuples that hash to it (1/nparts of
+   the keys); the listener map, liveness and the lowest NULL slot stay whole, so findtcb's
+   pass 2 (tcp_tcb.c:158-170) answers as against the whole table.  Every context still gets
+   every tcbs[] write (rxg_tcb_*).  A frame classified by the context of another queue
+   finds no exact TCB: steer with the NIC or with rxg_flow_part_of.  nparts = 1: the whole
+   table (the default).  Takes effect at the next sync (a table rebuild). */
+#define RXG_RSS_RETA_SIZE 128
+int rxg_flow_partition(rxg_ctx *ctx, uint32_t part, uint32_t nparts);
+/* The queue (0 .. nparts-1) an IPv4/TCP frame belongs to (frame bytes 26..37, read as the
+   kernel reads them: bytes at or past len are zero); 0 for other frames, which no context
+   looks up.  -EINVAL for frame NULL with len > 0 or nparts 0. */
+int rxg_flow_part_of(const uint8_t *frame, uint32_t len, uint32_t nparts);
+/* The Toeplitz RSS hash of 12 wire bytes (src ip | dst ip | src port | dst port). */
+uint32_t rxg_rss_hash(const uint8_t tuple12[12]);
+/* Distinct tuples in the context's device table (after the last sync); -EINVAL for NULL. */
+int64_t rxg_tcb_keys(rxg_ctx *ctx);
+
 /* Writes from other threads.  The calls above belong to the rx thread (the one running
    bursts and rxg_rx_replay, whose tcpswitch handlers write tcbs[] on the reference's rx
    lcore).  The reference's socket API writes tcbs[] from the application lcore, unlocked

@@ -1,0 +1,100 @@
+"""Flow-affinity sharding on the GPU (rxg_flow_partition): n contexts, each the
+rx queue of one RSS partition with 1/n of the exact-tuple table, classify the frames steered
+to them exactly as one context over the whole table does (the oracle, tcp_tcb.c:127-173):
+listeners, the NULL slot in front of a listener, duplicate tuples, host-order dst, bad int
+ports -- before and after mirror writes applied to every context."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import pktgen
+import rxg
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_parts(engines, frames, tcb, live, rec_kind):
+    n = len(engines)
+    parts = [rxg.flow_part_of(f, n) for f in frames]
+    for p, eng in enumerate(engines):
+        idx = [i for i, q in enumerate(parts) if q == p]
+        sub = [frames[i] for i in idx]
+        arena, off, lens = pktgen.pack_arena(sub)
+        eng.counters_reset()
+        got = eng.rx_arena(arena, off, lens, rec_kind)
+        exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+        exp = rxg.rec8_pack(exp["c"]) if rec_kind == rxg.REC8 else exp["c"]
+        assert got.tobytes() == exp.tobytes(), f"partition {p} of {n}: records differ"
+        assert np.array_equal(eng.counters(), ecnt), f"partition {p} of {n}: counters differ"
+    return parts
+
+
+@pytest.mark.parametrize("nparts", [2, 3])
+@pytest.mark.parametrize("rec_kind", [rxg.REC8, rxg.REC16])
+def test_flow_partitions_equal_whole_table(nparts, rec_kind):
+    rows, frames = pktgen.parity_set(seed=60 + nparts, n=6000, nflows=2000)
+    tcb, live = pktgen.table_arrays(rows)
+    engines = [rxg.Engine(device=0) for _ in range(nparts)]
+    whole = rxg.Engine(device=0)
+    try:
+        whole.tcb_load(tcb, live)
+        whole.tcb_sync()
+        for p, eng in enumerate(engines):
+            eng.flow_partition(p, nparts)
+            eng.tcb_load(tcb, live)
+            eng.tcb_sync()
+        keys = [eng.tcb_keys() for eng in engines]
+        assert sum(keys) == whole.tcb_keys()               # every tuple in exactly one table
+        assert min(keys) > 0.7 * whole.tcb_keys() / nparts  # and spread over them
+        parts = _run_parts(engines, frames, tcb, live, rec_kind)
+        assert len(set(parts)) == nparts
+
+        # mirror writes, applied to every context: a new child on the listener's port, a
+        # removed flow, a state change, the NULL slot in front of :8080 filled (the pass-2
+        # NULL flag moves), a re-tupled slot
+        rng = random.Random(nparts)
+        tl = [list(r) if r is not None else None for r in rows]
+        writes = []
+        for k in range(40):
+            i = rng.randrange(1, len(tl))
+            if tl[i] is None:
+                continue
+            if k % 3 == 0:
+                writes.append(("remove", i))
+                tl[i] = None
+            elif k % 3 == 1:
+                writes.append(("state", i, pktgen.LISTENING if k % 2 else pktgen.ESTABLISHED))
+                tl[i][4] = writes[-1][2]
+            else:
+                t = (80, 30000 + k, tl[i][2], pktgen.ip4(10, 200, k, 1), pktgen.ESTABLISHED)
+                writes.append(("upsert", i, t))
+                tl[i] = list(t)
+        nul = next(i for i, r in enumerate(tl) if r is None)
+        t = (9090, 1, pktgen.raw_of_host(pktgen.ip4(192, 168, 78, 2)), pktgen.ip4(10, 1, 2, 3), pktgen.ESTABLISHED)
+        writes.append(("upsert", nul, t))
+        tl[nul] = list(t)
+        for eng in engines:
+            for w in writes:
+                if w[0] == "remove":
+                    eng.tcb_remove(w[1])
+                elif w[0] == "state":
+                    eng.tcb_set_state(w[1], w[2])
+                else:
+                    d, s, dst, src, st = w[2]
+                    eng.tcb_upsert(w[1], d, s, dst, src, st, identifier=(w[1] % 65535) + 1)
+            eng.tcb_sync()
+        rows2 = [tuple(r) if r is not None else None for r in tl]
+        tcb2, live2 = pktgen.table_arrays(rows2)
+        _run_parts(engines, frames, tcb2, live2, rec_kind)
+    finally:
+        for eng in engines:
+            eng.close()
+        whole.close()
+
+
+def test_flow_partition_rejects_bad_arguments(engine):
+    for part, n in ((0, 0), (3, 3), (0, rxg.RSS_RETA_SIZE + 1)):
+        with pytest.raises(rxg.RxgError):
+            engine.flow_partition(part, n)
