@@ -1385,9 +1385,9 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
 
 template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
           bool DEFER = false, bool DTOP = true, int WPE = 0>
-// WPE 0: 3 waves per SIMD (at most 168 VGPRs) for the software-pipelined rounds, which
-// would otherwise take 170 and drop to 2; no bound for the forms without them
-__global__ __launch_bounds__(256, WPE ? WPE : (((STRIP & 8192) || MULTI || DEFER || MODE == 48) ? 1 : 3)) void rx_kernel(RxArgs a)
+// WPE 0: no bound, except 3 waves per SIMD (at most 168 VGPRs) for rx kernels with the
+// software-pipelined rounds (experiment STRIP 32768), which would otherwise take 170 and drop to 2
+__global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx_kernel(RxArgs a)
 {
     static_assert(!DEFER || MODE == 8 || MODE == 16, "deferred phase B: REC8 / REC16 only");
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -1500,7 +1500,10 @@ __global__ __launch_bounds__(256, WPE ? WPE : (((STRIP & 8192) || MULTI || DEFER
         // (experiment) = the round-2 form.  Multi-burst kernels keep that form: with the burst
         // table held in lanes the pipelined rounds need 176 VGPRs (2 waves per SIMD); so do
         // 48-byte records (168 with 16 B/lane spilled).
-        constexpr bool PIPE = !(STRIP & 8192) && !MULTI && !DEFER && MODE != 48;
+        // tx only (MODE 0, 101 VGPRs): in rx, at the occupancy grid, the second buffer's
+        // register cap cost more than the overlap gained; STRIP 32768
+        // (experiment) pipelines rx too, STRIP 8192 (experiment) turns it off in tx.
+        constexpr bool PIPE = !(STRIP & 8192) && !MULTI && !DEFER && (MODE == 0 || (STRIP & 32768));
         if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false, 0, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false, 0, PIPE>(a, cls, off, len, lane, sf);
@@ -1760,7 +1763,7 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         // 27: each lane loads its own TCB bucket (the round-1 form)
         case 27: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 4096>), dim3(blocks), dim3(256), 0, st, a); break;
         // 42: streaming-class rounds not pipelined (the round-2 form)
-        case 42: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 8192>), dim3(blocks), dim3(256), 0, st, a); break;
+        case 42: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 32768>), dim3(blocks), dim3(256), 0, st, a); break;
         // 4 waves per SIMD (at most 128 VGPRs) with the 8-slot ring (4 workgroups per CU fit in LDS)
         case 34: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
@@ -1785,12 +1788,12 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 8, false, false, true>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
-        if (L.variant == 42 && a.nbursts == 1) {  // streaming-class rounds not pipelined (round 2)
-            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 8192>), dim3(blocks), dim3(256), 0, st, a);
+        if (L.variant == 42 && a.nbursts == 1) {  // streaming-class rounds pipelined, 168 VGPRs
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 32768>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 43 && a.nbursts == 1) {  // pipelined at its natural 170 VGPRs, 2 waves per SIMD
-            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, true, 1>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 32768, false, 11, false, false, true, 1>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 34 && a.nbursts == 1) {
