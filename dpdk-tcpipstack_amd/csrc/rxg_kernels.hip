@@ -1010,6 +1010,72 @@ __device__ __forceinline__ void probe_issue_lds(const RxArgs &a, const Fields &F
     }
 }
 
+// Class 0 (frames <= 64 B) of a mixed slice by LDS-DMA (experiment STRIP 16384):
+// its 16-frames-per-instruction loads (lane l: one chunk of frame 16j + l/4) go straight into
+// the 4 KiB transpose area as the slice starts, the streaming classes run while they land,
+// and class 0 is computed last from LDS.  Lane l of instruction j lands at byte 1024j + 16l,
+// so it fetches the chunk the XOR swizzle of transpose_small_slice puts there.  The
+// compaction is recomputed at the end from the class's lane mask.
+__device__ __forceinline__ void class0_compact(unsigned long long m, uint32_t off, uint32_t len, int lane,
+                                               uint32_t &corig, uint32_t &coff, uint32_t &clen)
+{
+    corig = (uint32_t)lane; coff = off; clen = len;
+    if (m != ~0ull) {
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t dst = ((m >> lane) & 1ull) ? below : cnt + ((uint32_t)lane - below);
+        corig = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), lane);
+        coff = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)off);
+        clen = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)len);
+    }
+}
+__device__ __forceinline__ void class0_issue_lds(const RxArgs &a, unsigned long long m, uint32_t off, uint32_t len,
+                                                 int lane, uint32_t *t)
+{
+    uint32_t corig, coff, clen;
+    class0_compact(m, off, len, lane, corig, coff, clen);
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    const int slot = lane & 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int fr = 16 * j + (lane >> 2);
+        const int ch = slot ^ ((fr >> 2) & 3);
+        const uint32_t foff = lane_read(coff, fr), flen = lane_read(clen, fr);
+        const bool ok = (uint32_t)fr < cnt && (uint32_t)(ch * 16) < flen;
+        const uint8_t *g = ok ? a.frames + (size_t)foff * 64u + ch * 16 : a.frames;
+        const uint32_t lds = (uint32_t)(uintptr_t)(lds_void_t *)(t + j * 256);
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
+                     : "memory");
+    }
+}
+template <int MODE>
+__device__ __forceinline__ void class0_finish_lds(const RxArgs &a, unsigned long long m, uint32_t off, uint32_t len,
+                                                  int lane, uint32_t *sf, const uint32_t *t)
+{
+    // opaque copies: otherwise the compaction is CSE'd with the issue's and its three results
+    // stay live across the streaming classes
+    asm volatile("" : "+v"(lane), "+v"(off), "+v"(len));
+    uint32_t corig, coff, clen;
+    class0_compact(m, off, len, lane, corig, coff, clen);
+    const bool act = (uint32_t)lane < (uint32_t)__popcll(m);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA is not visible to the compiler
+    const uint4 *tq = reinterpret_cast<const uint4 *>(t);
+    const int sw = (lane >> 2) & 3;
+    uint32_t d[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint4 q = tq[lane * 4 + (c ^ sw)];
+        d[c][0] = q.x; d[c][1] = q.y; d[c][2] = q.z; d[c][3] = q.w;
+    }
+    const Fields F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)coff * 64u, act ? clen : 0u, d);
+    if constexpr (MODE != 0) {
+        if (act) park_fields<MODE>(sf, corig, F);
+    }
+    __builtin_amdgcn_wave_barrier();  // reads done before the LDS is reused
+}
 __device__ __forceinline__ void probe_lds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ Probe probe_from_lds(const RxArgs &a, const Fields &F, const uint4 (*pb)[64], int lane)
@@ -1504,7 +1570,15 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         // register cap cost more than the overlap gained; STRIP 32768
         // (experiment) pipelines rx too, STRIP 8192 (experiment) turns it off in tx.
         constexpr bool PIPE = !(STRIP & 8192) && !MULTI && !DEFER && (MODE == 0 || (STRIP & 32768));
-        if constexpr ((CMASK >> 0) & 1) run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
+        // STRIP 16384 (experiment): class 0 by LDS-DMA, computed after the streaming classes
+        constexpr bool C0DMA = (STRIP & 16384) != 0 && (CMASK & 1) != 0;
+        uint32_t *const t0 = sf + (MODE == 0 ? 0 : MODE == 48 ? NF48 * 64 : NF16 * 64);
+        const unsigned long long m0 = C0DMA ? __ballot(cls == 0) : 0ull;
+        if constexpr (C0DMA) {
+            if (m0 != 0ull) class0_issue_lds(a, m0, off, len, lane, t0);
+        } else if constexpr ((CMASK >> 0) & 1) {
+            run_class<0, 1, 4, false, MODE, false, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
+        }
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, false, 0, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, false, 0, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
@@ -1514,6 +1588,9 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 7) & 1) run_class<7, 64, 2, true, MODE, NT>(a, cls, off, len, lane, sf);
+        if constexpr (C0DMA) {
+            if (m0 != 0ull) class0_finish_lds<MODE>(a, m0, off, len, lane, sf, t0);
+        }
         if constexpr (MODE == 0 || (STRIP & 8)) {
             wcount(wc, RXG_C_RX, valid);
         } else if constexpr (DEFER) {
@@ -1790,6 +1867,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 42 && a.nbursts == 1) {  // streaming-class rounds pipelined, 168 VGPRs
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 32768>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 44 && a.nbursts == 1) {  // class 0 by LDS-DMA after the streaming classes
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 16384>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 43 && a.nbursts == 1) {  // pipelined at its natural 170 VGPRs, 2 waves per SIMD
