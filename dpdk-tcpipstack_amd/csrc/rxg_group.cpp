@@ -227,6 +227,12 @@ extern "C" int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32
         if (rc < 0) return rc;
     }
     const uint32_t k = (uint32_t)g->m.size();
+    for (uint32_t i = 0; i < k; ++i) {  // contiguous shards need every member's whole table
+        uint32_t part = 0, nparts = 1;
+        if (rxg_flow_partition_get(g->m[i], &part, &nparts) == 0 && nparts > 1)
+            return gfail(-EINVAL, "rxg_group_rx_burst: member %u is flow-partitioned (%u of %u); a group "
+                                  "cuts contiguous shards and needs whole tables", i, part, nparts);
+    }
     const uint32_t per = (n + k - 1) / k;
     g->shard_off.assign(k, 0);
     g->shard_n.assign(k, 0);

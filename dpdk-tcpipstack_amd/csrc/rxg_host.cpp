@@ -418,6 +418,14 @@ extern "C" int rxg_flow_partition(rxg_ctx *c, uint32_t part, uint32_t nparts)
     return 0;
 }
 
+extern "C" int rxg_flow_partition_get(rxg_ctx *c, uint32_t *part, uint32_t *nparts)
+{
+    if (!c || !part || !nparts) return fail(-EINVAL, "rxg_flow_partition_get: NULL argument");
+    *part = c->mir.part;
+    *nparts = c->mir.nparts;
+    return 0;
+}
+
 extern "C" uint32_t rxg_rss_hash(const uint8_t tuple12[12]) { return tuple12 ? rss_toeplitz(tuple12, 12) : 0u; }
 
 extern "C" int rxg_flow_part_of(const uint8_t *f, uint32_t len, uint32_t nparts)

@@ -215,6 +215,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_tcb_sync": (C.c_int, [vp]),
         "rxg_tcb_count": (i32, [vp]),
         "rxg_flow_partition": (C.c_int, [vp, u32, u32]),
+        "rxg_flow_partition_get": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32)]),
         "rxg_flow_part_of": (C.c_int, [C.c_char_p, u32, u32]),
         "rxg_rss_hash": (u32, [C.c_char_p]),
         "rxg_tcb_keys": (C.c_int64, [vp]),

@@ -267,6 +267,9 @@ int32_t rxg_tcb_count(rxg_ctx *ctx);
    table (the default).  Takes effect at the next sync (a table rebuild). */
 #define RXG_RSS_RETA_SIZE 128
 int rxg_flow_partition(rxg_ctx *ctx, uint32_t part, uint32_t nparts);
+/* The context's partition (1 of 1 when not partitioned).  A group (rxg_group_*) cuts
+   contiguous shards, so rxg_group_rx_burst refuses partitioned members (-EINVAL). */
+int rxg_flow_partition_get(rxg_ctx *ctx, uint32_t *part, uint32_t *nparts);
 /* The queue (0 .. nparts-1) an IPv4/TCP frame belongs to (frame bytes 26..37, read as the
    kernel reads them: bytes at or past len are zero); 0 for other frames, which no context
    looks up.  -EINVAL for frame NULL with len > 0 or nparts 0. */

@@ -94,6 +94,19 @@ def test_flow_partitions_equal_whole_table(nparts, rec_kind):
         whole.close()
 
 
+def test_group_refuses_partitioned_members():
+    rows, frames = pktgen.parity_set(seed=70, n=200)
+    tcb, live = pktgen.table_arrays(rows)
+    with rxg.Group([0, 0], max_batch=4096, max_bytes=8 << 20) as g:
+        g.tcb_load(tcb, live)
+        g.rx_burst(frames, rxg.REC16)  # whole tables: fine
+        g.members[1].flow_partition(1, 2)
+        with pytest.raises(rxg.RxgError, match="flow-partitioned"):
+            g.rx_burst(frames, rxg.REC16)
+        g.members[1].flow_partition(0, 1)
+        g.rx_burst(frames, rxg.REC16)
+
+
 def test_flow_partition_rejects_bad_arguments(engine):
     for part, n in ((0, 0), (3, 3), (0, rxg.RSS_RETA_SIZE + 1)):
         with pytest.raises(rxg.RxgError):
