@@ -430,7 +430,8 @@ extern "C" uint32_t rxg_rss_hash(const uint8_t tuple12[12]) { return tuple12 ? r
 
 extern "C" int rxg_flow_part_of(const uint8_t *f, uint32_t len, uint32_t nparts)
 {
-    if ((!f && len) || nparts == 0) return fail(-EINVAL, "rxg_flow_part_of: frame NULL or nparts 0");
+    if ((!f && len) || nparts == 0 || nparts > RXG_RSS_RETA_SIZE)
+        return fail(-EINVAL, "rxg_flow_part_of: frame NULL or nparts %u outside 1..%u", nparts, RXG_RSS_RETA_SIZE);
     uint8_t b[38] = {0};
     std::memcpy(b, f, std::min<uint32_t>(len, 38u));
     // ether_in's demux and ip_in's protocol test (etherin.c:12-37, ip.c:19-42): only TCP

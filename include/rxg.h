@@ -272,7 +272,7 @@ int rxg_flow_partition(rxg_ctx *ctx, uint32_t part, uint32_t nparts);
 int rxg_flow_partition_get(rxg_ctx *ctx, uint32_t *part, uint32_t *nparts);
 /* The queue (0 .. nparts-1) an IPv4/TCP frame belongs to (frame bytes 26..37, read as the
    kernel reads them: bytes at or past len are zero); 0 for other frames, which no context
-   looks up.  -EINVAL for frame NULL with len > 0 or nparts 0. */
+   looks up.  -EINVAL for frame NULL with len > 0 or nparts outside 1..RXG_RSS_RETA_SIZE. */
 int rxg_flow_part_of(const uint8_t *frame, uint32_t len, uint32_t nparts);
 /* The Toeplitz RSS hash of 12 wire bytes (src ip | dst ip | src port | dst port). */
 uint32_t rxg_rss_hash(const uint8_t tuple12[12]);

@@ -57,8 +57,9 @@ def test_flow_part_of_non_tcp_and_truncated():
 
 
 def test_flow_part_of_rejects_bad_arguments():
-    with pytest.raises(rxg.RxgError):
-        rxg.flow_part_of(pktgen.frame(), 0)
+    for n in (0, rxg.RSS_RETA_SIZE + 1):
+        with pytest.raises(rxg.RxgError):
+            rxg.flow_part_of(pktgen.frame(), n)
 
 
 def test_flow_parts_balance():

@@ -111,3 +111,59 @@ def test_flow_partition_rejects_bad_arguments(engine):
     for part, n in ((0, 0), (3, 3), (0, rxg.RSS_RETA_SIZE + 1)):
         with pytest.raises(rxg.RxgError):
             engine.flow_partition(part, n)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_flow_partition_replay_sequential_equivalence(seed):
+    """Each RSS queue's burst + replay equals the reference loop run over that queue's packets
+    in order, the table changing inside the burst (SYN -> child TCB, SYN_RECV -> ESTABLISHED,
+    FIN -> CLOSED -> remove_tcb): the children's tuples hash to the queue of the SYN that made
+    them, so the partitioned mirror holds them."""
+    import ctypes as C
+
+    from test_gpu_replay import Model, scenario, sequential_reference
+    rows, frames = scenario(seed, n=1200)
+    nparts = 2
+    for p in range(nparts):
+        mine = [f for f in frames if rxg.flow_part_of(f, nparts) == p]
+        exp, ecnt, erows = sequential_reference(rows, mine)
+        tcb, live = pktgen.table_arrays(rows)
+        with rxg.Engine(device=0, max_batch=4096, max_bytes=8 << 20) as eng:
+            eng.flow_partition(p, nparts)
+            eng.tcb_load(tcb, live)
+            eng.tcb_sync()
+            eng.counters_reset()
+            recs = eng.rx_burst(mine, rxg.REC16)
+            model = Model(rows, eng)
+            bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in mine]
+            addr = {C.addressof(b): i for i, b in enumerate(bufs)}
+            got = [None] * len(mine)
+
+            def free_mbuf(u, m):
+                i = addr[m]
+                if got[i] is None:
+                    got[i] = ("free",)
+
+            def rst(u, ip, tcp):
+                got[addr[ip - 14]] = ("rst",)
+
+            def tcpswitch(u, idx, st, tcp, ip, m):
+                i = addr[m]
+                got[i] = ("switch", idx, st)
+                model.handle(idx, st, mine[i])
+                return 0
+
+            ops = rxg.HandoffOps(None, rxg.HANDOFF_FREE(free_mbuf), rxg.HANDOFF_ARP_IN(), rxg.HANDOFF_GET_MAC(),
+                                 rxg.HANDOFF_ADD_MAC(), rxg.HANDOFF_SEND_RESET(rst), rxg.HANDOFF_ON_SEGMENT(),
+                                 rxg.HANDOFF_TCPSWITCH(tcpswitch))
+            ptrs = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
+            lib = rxg.load_library()
+            rc = lib.rxg_rx_replay(eng.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, len(bufs), 16)
+            assert rc == 0, lib.rxg_last_error()
+            for i, (v, idx, st) in enumerate(exp):
+                if v == rxg.V_DISPATCH:
+                    assert got[i] == ("switch", idx, st), (p, i, got[i], exp[i])
+                elif v in (rxg.V_RST_NOPCB, rxg.V_RST_LISTEN_NONSYN):
+                    assert got[i] == ("rst",), (p, i, got[i], exp[i])
+            assert model.rows == erows
+            assert eng.counters().tolist() == ecnt.tolist()
