@@ -437,7 +437,7 @@ extern "C" int rxg_flow_part_of(const uint8_t *f, uint32_t len, uint32_t nparts)
     // ether_in's demux and ip_in's protocol test (etherin.c:12-37, ip.c:19-42): only TCP
     // over IPv4 reaches findtcb
     if (b[12] != 0x08 || b[13] != 0x00 || b[23] != RXG_IPPROTO_TCP) return 0;
-    return (int)rss_queue(rss_toeplitz(b + 26, 12), nparts);
+    return (int)rss_queue(rss_toeplitz12(b + 26), nparts);
 }
 
 extern "C" int64_t rxg_tcb_keys(rxg_ctx *c) { return c ? (int64_t)c->mir.nkeys() : -EINVAL; }

@@ -71,3 +71,14 @@ def test_flow_parts_balance():
         for src, sport, dport in flows:
             cnt[rxg.flow_part_of(pktgen.frame(src_ip=src, sport=sport, dport=dport), n)] += 1
         assert min(cnt) > 0.75 * len(flows) / n, cnt
+
+
+def test_flow_part_of_table_equals_bitwise_hash():
+    """rxg_flow_part_of (byte tables) against rxg_rss_hash (the bit-serial definition) on
+    random tuples, through the whole 128-entry redirection table."""
+    rng = random.Random(11)
+    base = bytearray(pktgen.frame(sport=1, dport=2))
+    for _ in range(2000):
+        w = rng.randbytes(12)
+        base[26:38] = w
+        assert rxg.flow_part_of(bytes(base), rxg.RSS_RETA_SIZE) == rxg.rss_hash(w) % rxg.RSS_RETA_SIZE
