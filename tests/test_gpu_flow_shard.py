@@ -167,3 +167,70 @@ def test_flow_partition_replay_sequential_equivalence(seed):
                     assert got[i] == ("rst",), (p, i, got[i], exp[i])
             assert model.rows == erows
             assert eng.counters().tolist() == ecnt.tolist()
+
+
+def _rss_tables():
+    """T[i][v]: the RSS hash of 12 bytes holding v at position i (the hash is linear over
+    GF(2), so a tuple's hash is the XOR of its bytes' entries)."""
+    t = np.zeros((12, 256), dtype=np.uint32)
+    for i in range(12):
+        for v in range(256):
+            w = bytearray(12)
+            w[i] = v
+            t[i, v] = rxg.rss_hash(bytes(w))
+    return t
+
+
+def test_flow_partitions_c5_full_size():
+    """C5's scale (BASELINE.json configs[4]): 2^20 IMIX frames on 2^20 flows + a listener,
+    two RSS queues.  Each queue's context holds about half the million tuples and classifies
+    every frame steered to it to tcbs[1 + flow], ESTABLISHED, DISPATCH, both checksums 0."""
+    n, flows, nparts = 1 << 20, 1 << 20, 2
+    tcb, live = rxg.synthetic_tcb_table(flows)
+    gen = rxg.Engine(device=0)
+    parts = [rxg.Engine(device=0) for _ in range(nparts)]
+    try:
+        b = gen.synth(n=n, nflows=flows, mix=1, seed=0xF10, with_flows=True)
+        gen.sync()
+        fl = b["flow"].download(np.uint32, n)
+        lens = b["len"].download(np.uint16, n)
+        off = b["off64"].download(np.uint32, n)
+        arena = b["arena"].download(np.uint8, b["arena_bytes"])
+        # frame bytes 26..37 of every frame, then the queue by the byte tables
+        pos = off.astype(np.int64)[:, None] * 64 + np.arange(26, 38)[None, :]
+        w = arena[pos]
+        t = _rss_tables()
+        h = np.zeros(n, dtype=np.uint32)
+        for i in range(12):
+            h ^= t[i][w[:, i]]
+        q = (h % rxg.RSS_RETA_SIZE) % nparts
+        for k in range(0, n, 4099):  # spot-check the vectorised steering against the C ABI
+            f = arena[int(off[k]) * 64:int(off[k]) * 64 + int(lens[k])].tobytes()
+            assert rxg.flow_part_of(f, nparts) == q[k]
+        keys = []
+        for p, eng in enumerate(parts):
+            eng.flow_partition(p, nparts)
+            eng.tcb_load(tcb, live)
+            eng.tcb_sync()
+            keys.append(eng.tcb_keys())
+            sel = np.nonzero(q == p)[0]
+            m = len(sel)
+            d_off = eng.to_device(off[sel].copy())
+            d_len = eng.to_device(lens[sel].copy())
+            out = eng.alloc(m * rxg.REC16)
+            eng.counters_reset()
+            eng.rx_burst_dev(b["arena"].ptr, d_off.ptr, d_len.ptr, m, out.ptr, rxg.REC16)
+            eng.sync()
+            rec = out.download(rxg.REC16_DTYPE, m)
+            for a in (d_off, d_len, out):
+                a.free()
+            assert (rec["verdict"] == rxg.V_DISPATCH).all(), p
+            assert (rec["tcb_idx"] == fl[sel].astype(np.int64) + 1).all(), p
+            assert (rec["state"] == rxg.TCP_ESTABLISHED).all(), p
+            assert (rec["ip_cksum"] == 0).all() and (rec["tcp_cksum"] == 0).all(), p
+            assert (rec["datalen"] == lens[sel].astype(np.int64) - 54).all(), p
+        assert sum(keys) == flows + 1 and min(keys) > 0.45 * flows, keys
+    finally:
+        for eng in parts:
+            eng.close()
+        gen.close()
