@@ -1563,6 +1563,8 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
                                                              ? NF * 256 + 4096 : NF * 256, bc);
         // classes 0-2 of mixed slices: plain loads; STRIP 131072 (experiment): non-temporal
         constexpr bool NTS = NT && (STRIP & 131072) != 0;
+        // 257-576 B classes: non-temporal; STRIP 262144 (experiment): plain
+        constexpr bool NTM = NT && (STRIP & 262144) == 0;
         constexpr int SVS = (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0;
         // The streaming classes' rounds software-pipelined; STRIP 8192
         // (experiment) = the round-2 form.  Multi-burst kernels keep that form: with the burst
@@ -1583,8 +1585,8 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         }
         if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, NTS, 0, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, NTS, 0, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NTM, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NTM, SVS, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
         if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
@@ -1877,6 +1879,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 49 && a.nbursts == 1) {  // classes 0-2 of mixed slices non-temporal
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 131072>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 50 && a.nbursts == 1) {  // 257-576 B classes with plain loads
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 262144>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 43 && a.nbursts == 1) {  // pipelined at its natural 170 VGPRs, 2 waves per SIMD
