@@ -1292,7 +1292,7 @@ __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int l
     __builtin_amdgcn_wave_barrier();  // reads done before the LDS is reused
 }
 
-template <bool SEL, typename BC>
+template <bool SEL, typename BC, bool NTD = false>
 __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane, uint32_t &off, uint32_t &len, BC &bc)
 {
     // Unconditional loads of a clamped index (every burst has n >= 1), not masked here:
@@ -1304,8 +1304,13 @@ __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane,
     const uint32_t f = (su - bc.slice0_of(a, k)) * 64u + (uint32_t)lane;
     const uint32_t fc = min(f, bc.n_of(a, k) - 1u);
     const uint32_t pf = SEL ? a.sel[fc] : fc;
-    off = bc.off64_of(a, k)[pf];
-    len = bc.len_of(a, k)[pf];
+    if constexpr (NTD) {  // experiment (STRIP 524288): non-temporal descriptor loads
+        off = __builtin_nontemporal_load(bc.off64_of(a, k) + pf);
+        len = __builtin_nontemporal_load(bc.len_of(a, k) + pf);
+    } else {
+        off = bc.off64_of(a, k)[pf];
+        len = bc.len_of(a, k)[pf];
+    }
 }
 
 // Records of a wave's slices are staged in LDS and written out RS slices at a time (and
@@ -1436,7 +1441,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     const Probe PO = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, true, F);
     if (nxt) issue_small_slice<true>(a, n_off, n_len, lane, vb[1 - P]);
     uint32_t y_off, y_len;
-    load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
+    load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
     classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PO, wc, rec, fc, cached);
     bytes += c_len;
     if (!(STRIP & 4)) {
@@ -1492,8 +1497,8 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
     uint32_t c_off = 0, c_len = 0, n_off = 0, n_len = 0;
     BurstCursor<MULTI> bc;
     bc.load(a, lane);
-    load_desc<SEL>(a, s, lane, c_off, c_len, bc);
-    load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+    load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s, lane, c_off, c_len, bc);
+    load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s + nwaves, lane, n_off, n_len, bc);
     // DEFER: the slice whose phase B is pending (wave-uniform; ~0 = none), its fields
     uint32_t d_s = ~0u, d_len = 0u;
     bool d_issue = false;  // the pending slice's probe DMA is still to be issued
@@ -1550,7 +1555,7 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         // were still in flight there, where the register copies c <- n <- y made the wave
         // wait for them (an s_waitcnt vmcnt(0) per slice in the ISA).
         uint32_t y_off = 0u, y_len = 0u;
-        if constexpr (DTOP) load_desc<SEL>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
+        if constexpr (DTOP) load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
         if constexpr (DEFER) {
             if (d_issue) {
                 probe_issue_lds(a, dF, s_pb[wid]);
@@ -1636,7 +1641,7 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         if constexpr (DTOP) {
             n_off = y_off; n_len = y_len;
         } else {
-            load_desc<SEL>(a, s + nwaves, lane, n_off, n_len, bc);
+            load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s + nwaves, lane, n_off, n_len, bc);
         }
     }
     finish_pending();
@@ -1883,6 +1888,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 50 && a.nbursts == 1) {  // 257-576 B classes with plain loads
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 262144>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 51 && a.nbursts == 1) {  // non-temporal descriptor loads
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 524288>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 43 && a.nbursts == 1) {  // pipelined at its natural 170 VGPRs, 2 waves per SIMD
