@@ -88,14 +88,30 @@ struct rxg_ctx {
     int32_t dev_min_null = INT32_MAX;
     // Ordering of table writes against the kernels that read the tables:
     // mirror writes run on `stream`; a burst on another stream waits for mirror_ev, and the
-    // next mirror write waits for read_ev, recorded after a table-reading launch on a
-    // stream other than `stream`.
-    hipEvent_t mirror_ev = nullptr, read_ev = nullptr;
-    bool mirror_ev_set = false, read_ev_set = false;
-    MirrorPatch *h_patch = nullptr;  // pinned: the patch kernel reads it over PCIe
-    uint32_t h_patch_cap = 0;
-    hipEvent_t patch_ev = nullptr;   // the last patch kernel (h_patch is free after it)
-    bool patch_ev_set = false;
+    // next mirror write waits for every reader event: one per stream other than `stream`
+    // that launched a table-reading kernel since the last write, recorded after its latest
+    // such launch (one event per stream, so a reader on s1 followed by one on s2 are both
+    // waited for).
+    hipEvent_t mirror_ev = nullptr;
+    bool mirror_ev_set = false;
+    struct Reader {
+        hipStream_t s;
+        hipEvent_t e;
+        bool set;
+    };
+    std::vector<Reader> readers;
+    // Patch upload ring: the patch kernel reads its list from pinned host memory over PCIe,
+    // so a buffer is reused only after its kernel ran; kPatchBufs buffers, each with its
+    // event, and the host waits only when all of them are in flight (a patch kernel waits on
+    // the device for bursts running on caller streams, which can be long).
+    static constexpr int kPatchBufs = 4;
+    struct PatchBuf {
+        MirrorPatch *h = nullptr;
+        uint32_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool set = false;
+    } patch[kPatchBufs];
+    int patch_next = 0;
 
     unsigned long long *counters = nullptr;
 
@@ -254,9 +270,9 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
         delete c;
         return fail(-EIO, "rxg_init: hipStreamCreate failed");
     }
-    if (hipEventCreateWithFlags(&c->mirror_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->read_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->patch_ev, hipEventDisableTiming) != hipSuccess) {
+    bool ev_ok = hipEventCreateWithFlags(&c->mirror_ev, hipEventDisableTiming) == hipSuccess;
+    for (auto &pb : c->patch) ev_ok = ev_ok && hipEventCreateWithFlags(&pb.ev, hipEventDisableTiming) == hipSuccess;
+    if (!ev_ok) {
         rxg_fini(c);
         return fail(-EIO, "rxg_init: hipEventCreate failed");
     }
@@ -292,6 +308,8 @@ extern "C" int rxg_fini(rxg_ctx *c)
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &r : c->readers)  // table readers still running on caller streams
+        if (r.set) (void)hipEventSynchronize(r.e);
     for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket})
         if (b->p) (void)hipFree(b->p);
 #ifdef RXG_EXPERIMENTS
@@ -299,9 +317,12 @@ extern "C" int rxg_fini(rxg_ctx *c)
 #endif
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
-    if (c->h_patch) (void)hipHostFree(c->h_patch);
-    for (hipEvent_t e : {c->mirror_ev, c->read_ev, c->patch_ev})
-        if (e) (void)hipEventDestroy(e);
+    for (auto &pb : c->patch) {
+        if (pb.h) (void)hipHostFree(pb.h);
+        if (pb.ev) (void)hipEventDestroy(pb.ev);
+    }
+    for (auto &r : c->readers) (void)hipEventDestroy(r.e);
+    if (c->mirror_ev) (void)hipEventDestroy(c->mirror_ev);
     if (c->counters) (void)hipFree(c->counters);
     if (c->h_arena) (void)hipHostFree(c->h_arena);
     if (c->h_off) (void)hipHostFree(c->h_off);
@@ -478,13 +499,22 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
     return c->dirty ? tcb_push(c) : 0;
 }
 
-// Before a mirror write on c->stream: kernels that read the tables on another stream are done.
+// Before a mirror write on c->stream: kernels that read the tables on other streams are done.
 static int wait_table_readers(rxg_ctx *c)
 {
-    if (c->read_ev_set) {
-        HIP_OK(hipStreamWaitEvent(c->stream, c->read_ev, 0));
-        c->read_ev_set = false;
-    }
+    for (auto &r : c->readers)
+        if (r.set) {
+            HIP_OK(hipStreamWaitEvent(c->stream, r.e, 0));
+            r.set = false;
+        }
+    return 0;
+}
+
+// Before device table buffers are freed or reallocated: every reader has finished (host wait).
+static int sync_table_readers(rxg_ctx *c)
+{
+    for (auto &r : c->readers)
+        if (r.set) HIP_OK(hipEventSynchronize(r.e));
     return 0;
 }
 
@@ -494,22 +524,25 @@ static int apply_patches(rxg_ctx *c, M &mirror)
 {
     const std::vector<MirrorPatch> &p = mirror.patches;
     if (p.empty()) return 0;
-    if (c->patch_ev_set) HIP_OK(hipEventSynchronize(c->patch_ev));  // h_patch free again
-    if (p.size() > c->h_patch_cap) {
-        if (c->h_patch) HIP_OK(hipHostFree(c->h_patch));
-        c->h_patch = nullptr;
-        c->h_patch_cap = 0;
+    rxg_ctx::PatchBuf &pb = c->patch[c->patch_next];
+    c->patch_next = (c->patch_next + 1) % rxg_ctx::kPatchBufs;
+    if (pb.set) HIP_OK(hipEventSynchronize(pb.ev));  // this buffer's kernel has read it
+    pb.set = false;
+    if (p.size() > pb.cap) {
+        if (pb.h) HIP_OK(hipHostFree(pb.h));
+        pb.h = nullptr;
+        pb.cap = 0;
         const uint32_t cap = (uint32_t)std::max<size_t>(p.size() * 2, 1024);
-        HIP_OK(hipHostMalloc((void **)&c->h_patch, (size_t)cap * sizeof(MirrorPatch), hipHostMallocDefault));
-        c->h_patch_cap = cap;
+        HIP_OK(hipHostMalloc((void **)&pb.h, (size_t)cap * sizeof(MirrorPatch), hipHostMallocDefault));
+        pb.cap = cap;
     }
-    std::memcpy(c->h_patch, p.data(), p.size() * sizeof(MirrorPatch));
+    std::memcpy(pb.h, p.data(), p.size() * sizeof(MirrorPatch));
     int rc = wait_table_readers(c);
     if (rc) return rc;
-    HIP_OK(launch_mirror_patch(c->h_patch, (uint32_t)p.size(), (uint4 *)c->buckets.p, (int32_t *)c->listen.p,
+    HIP_OK(launch_mirror_patch(pb.h, (uint32_t)p.size(), (uint4 *)c->buckets.p, (int32_t *)c->listen.p,
                                (uint2 *)c->d_arp.p, c->stream));
-    HIP_OK(hipEventRecord(c->patch_ev, c->stream));
-    c->patch_ev_set = true;
+    HIP_OK(hipEventRecord(pb.ev, c->stream));
+    pb.set = true;
     HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
     c->mirror_ev_set = true;
     mirror.patches_taken();
@@ -530,7 +563,7 @@ static int tcb_push(rxg_ctx *c)
         const size_t sb = m.slots.size() * sizeof(Slot), lb = m.listen.size() * sizeof(int32_t);
         if (sb > c->buckets.bytes || lb > c->listen.bytes) {
             // the old buffers must be idle before they are freed
-            if (c->read_ev_set) HIP_OK(hipEventSynchronize(c->read_ev));
+            if ((rc = sync_table_readers(c))) return rc;
             HIP_OK(hipStreamSynchronize(c->stream));
             if ((rc = ensure(c->buckets, sb))) return rc;
             if ((rc = ensure(c->listen, lb))) return rc;
@@ -593,7 +626,7 @@ static int arp_sync(rxg_ctx *c)
         a.rebuild();
         const size_t bytes = a.slots.size() * 4;
         if (bytes > c->d_arp.bytes) {
-            if (c->read_ev_set) HIP_OK(hipEventSynchronize(c->read_ev));
+            if ((rc = sync_table_readers(c))) return rc;
             HIP_OK(hipStreamSynchronize(c->stream));
             if ((rc = ensure(c->d_arp, bytes))) return rc;
         }
@@ -618,12 +651,33 @@ static int order_table_reader_before(rxg_ctx *c, hipStream_t st)
     return 0;
 }
 
+static constexpr size_t kMaxReaderStreams = 16;
+
 static int order_table_reader_after(rxg_ctx *c, hipStream_t st)
 {
-    if (st != c->stream) {
-        HIP_OK(hipEventRecord(c->read_ev, st));
-        c->read_ev_set = true;
+    if (st == c->stream) return 0;
+    rxg_ctx::Reader *r = nullptr;
+    for (auto &x : c->readers)
+        if (x.s == st) r = &x;
+    if (!r) {
+        for (auto &x : c->readers)
+            if (!x.set) { r = &x; break; }
+        if (!r && c->readers.size() >= kMaxReaderStreams) {
+            // more reader streams than events: the next write's stream waits for them now
+            int rc = wait_table_readers(c);
+            if (rc) return rc;
+            r = &c->readers[0];
+        }
+        if (!r) {
+            hipEvent_t e;
+            HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->readers.push_back({st, e, false});
+            r = &c->readers.back();
+        }
+        r->s = st;
     }
+    HIP_OK(hipEventRecord(r->e, st));
+    r->set = true;
     return 0;
 }
 
@@ -659,6 +713,9 @@ static bool rec_kind_ok(uint32_t k) { return k == RXG_REC8 || k == RXG_REC16 || 
 static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
                          void *stream, const char *who)
 {
+    // a rejected launch leaves nothing to replay: rxg_rx_replay refuses until a burst succeeds
+    c->burst_ok = false;
+    c->last_bursts.clear();
     if (!rec_kind_ok(rec_kind)) return fail(-EINVAL, "%s: rec_kind %u", who, rec_kind);
     if (k && !bursts) return fail(-EINVAL, "%s: NULL burst table", who);
     bool any = false;

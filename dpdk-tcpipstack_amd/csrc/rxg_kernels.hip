@@ -128,12 +128,56 @@ __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__bui
 // slice0, n and pointers in VGPRs (loaded once per wave), so finding the burst of a slice is
 // one compare + ballot popcount and its fields are v_readlane -- no memory access and no
 // scalar-load wait per lookup.  Single-burst launches (MULTI false) read burst 0 directly.
+//
+// Work units.  A wave takes units u = wave, wave + nwaves, ...; in production a unit is a
+// slice.  Experiment STRIP 1048576 (variant 52, DESIGN.md §9 "Launch tail"): the slices of the
+// last, partial generation (nslices mod nwaves of them) are each cut into g <= kMaxPieces
+// pieces of w = ceil(64 / g) consecutive frames, g = nwaves / tail, so that generation spreads
+// over (nearly) every wave instead of a third of them at 2^20 frames.  Measured slower (C2
+// 22.6 against 19.5 us, C4 78.0 against 74.5): a piece costs about what a whole slice does
+// (its rounds are as many, its latency chain as long, and a 64 B piece leaves the prefetched
+// all-small path), so every wave pays a slice-time where a third of them did.  Dynamic claims
+// were not built: a returning device-scope atomicAdd on one word saturates at ≈88 claims/µs
+// (MI355X_MICROARCH.md, dequeue), ten times fewer than the 64 B burst's ≈860 slices/µs.
+constexpr uint32_t kMaxPieces = 4;
+
 template <bool MULTI>
 struct BurstCursor {
     uint32_t slice0 = 0, n = 0;
     const uint32_t *off64 = nullptr;
     const uint16_t *len = nullptr;
     uint8_t *out = nullptr;
+    // units (wave-uniform): [0, u_full) whole slices, then u_g pieces of u_w frames per slice
+    uint32_t u_full = 0, u_g = 1, u_w = 64, u_m = 0, u_n = 0;
+
+    __device__ __forceinline__ void units_init(uint32_t nslices, uint32_t nwaves, bool bal)
+    {
+        u_full = nslices; u_g = 1; u_w = 64; u_m = 0; u_n = nslices;
+        const uint32_t full = bal ? (nslices / nwaves) * nwaves : nslices;
+        const uint32_t tail = nslices - full;
+        if (tail == 0) return;
+        const uint32_t g = min(nwaves / tail, kMaxPieces);
+        if (g <= 1) return;
+        u_full = full;
+        u_g = g;
+        u_w = (64u + g - 1u) / g;
+        u_m = 0xFFFFFFFFu / g;  // q = umulhi(t, u_m) is t / g or one less
+        u_n = full + tail * g;
+    }
+    // unit u -> its launch slice, its first frame in the slice and its width (frames)
+    __device__ __forceinline__ void locate(uint32_t u, uint32_t &slice, uint32_t &lo, uint32_t &width) const
+    {
+        if (u < u_full) {
+            slice = u; lo = 0u; width = 64u;
+            return;
+        }
+        const uint32_t t = u - u_full;
+        uint32_t q = __umulhi(t, u_m);
+        if ((q + 1u) * u_g <= t) ++q;
+        slice = u_full + q;
+        lo = (t - q * u_g) * u_w;
+        width = min(u_w, 64u - lo);  // the last piece of a slice is the shorter one
+    }
 
     __device__ __forceinline__ void load(const RxArgs &a, int lane)
     {
@@ -187,12 +231,16 @@ struct BurstCursor {
     }
 };
 
-// Frames in launch slice s (64 except a burst's last slice).
+// Frames in work unit u (64 except a burst's last slice and the pieces of the last
+// generation; a piece past its slice's last frame has none).
 template <typename BC>
-__device__ __forceinline__ uint32_t slice_frames(const RxArgs &a, uint32_t s, BC &bc)
+__device__ __forceinline__ uint32_t slice_frames(const RxArgs &a, uint32_t u, BC &bc)
 {
-    const uint32_t k = bc.of(a, s);
-    return min(64u, bc.n_of(a, k) - (s - bc.slice0_of(a, k)) * 64u);
+    uint32_t sl, lo, w;
+    bc.locate(u, sl, lo, w);
+    const uint32_t k = bc.of(a, sl);
+    const uint32_t sf = min(64u, bc.n_of(a, k) - (sl - bc.slice0_of(a, k)) * 64u);
+    return lo < sf ? min(w, sf - lo) : 0u;
 }
 
 // One frame's record as classify computes it (16 or 48 bytes, rxg.h rxg_rec16/rxg_rec48).
@@ -1299,9 +1347,11 @@ __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane,
     // masking would consume the load at once, and s_waitcnt retires in order, so the wait
     // would also drain every older load in flight (the prefetched frames of the small-slice
     // pipeline).  Callers treat lanes past their burst's n (slice_frames) as invalid.
-    const uint32_t su = uniform(min(s, a.nslices - 1u));
-    const uint32_t k = bc.of(a, su);
-    const uint32_t f = (su - bc.slice0_of(a, k)) * 64u + (uint32_t)lane;
+    const uint32_t su = uniform(min(s, bc.u_n - 1u));
+    uint32_t sl, lo, w;
+    bc.locate(su, sl, lo, w);
+    const uint32_t k = bc.of(a, sl);
+    const uint32_t f = (sl - bc.slice0_of(a, k)) * 64u + lo + (uint32_t)lane;
     const uint32_t fc = min(f, bc.n_of(a, k) - 1u);
     const uint32_t pf = SEL ? a.sel[fc] : fc;
     if constexpr (NTD) {  // experiment (STRIP 524288): non-temporal descriptor loads
@@ -1368,10 +1418,11 @@ struct RecRing {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t sl = uniform(base[i]);
+            uint32_t sl, lo, w;
+            bc.locate(uniform(base[i]), sl, lo, w);
             const uint32_t kb = bc.of(a, sl);
-            const uint32_t f0 = (sl - bc.slice0_of(a, kb)) * 64u;  // first frame of the slice in its burst
-            const uint32_t nb = bc.n_of(a, kb);
+            const uint32_t f0 = (sl - bc.slice0_of(a, kb)) * 64u + lo;  // first frame of the unit in its burst
+            const uint32_t nb = min(bc.n_of(a, kb), f0 + w);
             if constexpr (MODE == 8) {  // 64 lanes x 8 B: 512 B contiguous per instruction
                 uint2 *d8 = reinterpret_cast<uint2 *>(bc.out_of(a, kb) + (size_t)f0 * 8u);
                 if (f0 + (uint32_t)lane < nb) {
@@ -1479,7 +1530,6 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
     const int wid = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
     const uint32_t nwaves = gridDim.x * 4u;
-    const uint32_t nslices = a.nslices;
 
     WaveCounters wc;
 #pragma unroll
@@ -1497,6 +1547,9 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
     uint32_t c_off = 0, c_len = 0, n_off = 0, n_len = 0;
     BurstCursor<MULTI> bc;
     bc.load(a, lane);
+    // work units: whole slices; STRIP 1048576 (experiment) = the last generation's slices in pieces
+    bc.units_init(a.nslices, nwaves, (STRIP & 1048576) != 0);
+    const uint32_t nslices = bc.u_n;  // units from here on
     load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s, lane, c_off, c_len, bc);
     load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s + nwaves, lane, n_off, n_len, bc);
     // DEFER: the slice whose phase B is pending (wave-uniform; ~0 = none), its fields
@@ -1852,6 +1905,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         case 42: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 32768>), dim3(blocks), dim3(256), 0, st, a); break;
         // 4 waves per SIMD (at most 128 VGPRs) with the 8-slot ring (4 workgroups per CU fit in LDS)
         case 34: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 8, false, false, true, 4>), dim3(blocks), dim3(256), 0, st, a); break;
+        // 52: the last generation's slices cut into pieces
+        case 52: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
             if (a.nbursts > 1)
                 hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
@@ -1888,6 +1943,13 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         }
         if (L.variant == 50 && a.nbursts == 1) {  // 257-576 B classes with plain loads
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 262144>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 52) {  // the last generation's slices cut into pieces
+            if (a.nbursts > 1)
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 51 && a.nbursts == 1) {  // non-temporal descriptor loads
@@ -1947,6 +2009,8 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 1024>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 22)  // whole 128-byte first lines rewritten
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 256>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 52)  // the last generation's slices cut into pieces
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 32)  // descriptors loaded at the slice's end (round-2 start)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
         else

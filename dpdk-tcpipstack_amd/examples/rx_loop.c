@@ -37,6 +37,9 @@ struct out_rec {
 };
 
 static struct row *tcbs;  /* tcbs[] and Ntcb of tcp_tcb.c:21-22 */
+/* Defined here because this program links none of the reference's objects.  In the patched
+   stack tcp_in.c (tcp_in.c:18-19) keeps defining them and the patch only declares them, through
+   tcp_in.h:7,11. */
 int tcpchecksumerror;     /* tcp_in.c:18, extern in tcp_in.h:7 */
 int tcpnopcb;             /* tcp_in.c:19, extern in tcp_in.h:11 */
 static int32_t ntcb, cap;
