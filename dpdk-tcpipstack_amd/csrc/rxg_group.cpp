@@ -1,16 +1,21 @@
 // rxg_group.cpp — several GPUs behind one rx loop.
 //
 // A group is one rxg context per device.  Every context holds a full replica of the TCB
-// mirror (tcbs[] writes are applied to all of them), a host-buffer burst is cut into one
-// contiguous shard per member and the shards run concurrently (one host thread per member,
-// each on its own device and stream), and the records come back in packet order.  The
+// mirror (tcbs[] writes are applied to all of them), a burst is cut into one contiguous
+// shard per member and the shards run concurrently -- a host-buffer burst on the group's
+// worker threads (one per member, kept for the group's life), a device-resident burst
+// (rxg_group_rx_burst_dev) as one asynchronous launch per member -- each member on its own
+// device and stream, and the records come back in packet order.  The
 // replay then walks the members' shards in packet order: a handler's tcbs[] write, mirrored
 // through the group, reaches every member before that member's shard is replayed, and
 // rxg_rx_replay re-classifies the shard's affected packets as it does within one burst, so
 // the group is sequentially equivalent to ether_in over the whole burst.
 //
-// Built on the public C ABI only (include/rxg.h).
-#include <rccl/rccl.h>
+// Built on the public C ABI only (include/rxg.h).  RCCL is loaded at the first counter merge
+// over distinct GPUs (dlopen), so librxg.so does not need it at load time: single-GPU users
+// and the plain-C rx loop never touch it.
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only; the functions come from dlopen("librccl.so")
 
 #include <cerrno>
 #include <cstdarg>
@@ -18,11 +23,14 @@
 #include <cstring>
 #include <set>
 #include <string>
+#include <mutex>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "rxg.h"
 #include "rxg_opqueue.h"
+#include "rxg_packpool.h"
 
 struct rxg_group {
     std::vector<rxg_ctx *> m;
@@ -38,9 +46,13 @@ struct rxg_group {
     // distinct GPUs, set up at the first rxg_group_counters_read; the all-reduce writes into
     // `merged` (one counter block per member), never into the members' own blocks
     std::vector<int32_t> devices;
-    int rccl = -1;  // -1 not tried, 0 host sum (members share a GPU), 1 RCCL
+    int rccl = -1;  // -1 not tried, 0 host sum (members share a GPU, or RCCL unavailable), 1 RCCL
+    std::string rccl_why;  // why the merge is on the host
     std::vector<ncclComm_t> comms;
     std::vector<void *> merged;
+    // host-buffer bursts: member i > 0 runs its shard on worker thread i, kept for the
+    // group's life (no thread is created per burst); member 0 on the caller's thread
+    rxg::PackPool workers;
 };
 
 namespace {
@@ -118,10 +130,60 @@ extern "C" int rxg_group_init(const int32_t *devices, uint32_t ndev, const rxg_c
     return 0;
 }
 
+// ------------------------------------------------------------------------ RCCL ---
+// The few RCCL entry points the merge uses, resolved once from librccl.so.
+namespace {
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string why;
+    ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+std::mutex g_rccl_mu;
+Rccl g_rccl;
+
+template <typename F>
+bool rccl_sym(void *h, F &fn, const char *name, std::string &why)
+{
+    fn = reinterpret_cast<F>(dlsym(h, name));
+    if (!fn) why = std::string("librccl.so has no ") + name;
+    return fn != nullptr;
+}
+
+const Rccl &rccl_lib()
+{
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    Rccl &r = g_rccl;
+    if (r.tried) return r;
+    r.tried = true;
+    void *h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        const char *e = dlerror();
+        r.why = std::string("dlopen librccl.so: ") + (e ? e : "not found");
+        return r;
+    }
+    bool ok = true;
+    ok &= rccl_sym(h, r.CommInitAll, "ncclCommInitAll", r.why);
+    ok &= rccl_sym(h, r.CommDestroy, "ncclCommDestroy", r.why);
+    ok &= rccl_sym(h, r.GroupStart, "ncclGroupStart", r.why);
+    ok &= rccl_sym(h, r.GroupEnd, "ncclGroupEnd", r.why);
+    ok &= rccl_sym(h, r.AllReduce, "ncclAllReduce", r.why);
+    ok &= rccl_sym(h, r.GetErrorString, "ncclGetErrorString", r.why);
+    r.ok = ok;
+    return r;
+}
+}  // namespace
+
 extern "C" int rxg_group_fini(rxg_group *g)
 {
     if (!g) return 0;
-    for (ncclComm_t c : g->comms) (void)ncclCommDestroy(c);
+    for (ncclComm_t c : g->comms) (void)rccl_lib().CommDestroy(c);
     for (size_t i = 0; i < g->merged.size(); ++i)
         if (g->merged[i]) (void)rxg_dev_free(g->m[i], g->merged[i]);
     for (rxg_ctx *c : g->m) rxg_fini(c);
@@ -245,19 +307,65 @@ extern "C" int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32
     g->burst_ok = false;
     std::vector<int> rc(k, 0);
     std::vector<std::string> err(k);
-    auto run = [&](uint32_t i) {
+    g->workers.run(k, [&](uint32_t i) {
         rc[i] = rxg_rx_burst(g->m[i], pkts + g->shard_off[i], g->shard_n[i], rec_kind,
                              (uint8_t *)out_host + (size_t)g->shard_off[i] * rec_kind);
         if (rc[i]) err[i] = rxg_last_error();  // thread-local in the member's thread
-    };
-    std::vector<std::thread> th;
-    for (uint32_t i = 1; i < k; ++i) th.emplace_back(run, i);
-    run(0);
-    for (auto &t : th) t.join();
+    });
     for (uint32_t i = 0; i < k; ++i)
         if (rc[i]) return gfail(rc[i], "member %u: %s", i, err[i].c_str());
     g->burst_ok = true;
     return 0;
+}
+
+// Device-resident group burst: shards[i] is member i's contiguous share of the burst, in
+// packet order, in memory that member's GPU reads.  One asynchronous launch per member (the
+// members' kernels run concurrently, each on its context's stream); rxg_group_sync waits.
+extern "C" int rxg_group_rx_burst_dev(rxg_group *g, const rxg_dev_batch *shards, uint32_t nshards)
+{
+    if (!g || (nshards && !shards)) return gfail(-EINVAL, "rxg_group_rx_burst_dev: NULL argument");
+    g->burst_ok = false;
+    const uint32_t k = (uint32_t)g->m.size();
+    if (nshards != k) return gfail(-EINVAL, "rxg_group_rx_burst_dev: %u shards for %u members", nshards, k);
+    const uint32_t kind = shards[0].rec_kind;
+    for (uint32_t i = 0; i < k; ++i)
+        if (shards[i].rec_kind != kind)  // the replay walks one record array of one stride
+            return gfail(-EINVAL, "rxg_group_rx_burst_dev: shard %u rec_kind %u, shard 0 %u", i,
+                         shards[i].rec_kind, kind);
+    {
+        const int rc = rxg_group_tcb_drain(g);
+        if (rc < 0) return rc;
+    }
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        uint32_t part = 0, nparts = 1;
+        if (rxg_flow_partition_get(g->m[i], &part, &nparts) == 0 && nparts > 1)
+            return gfail(-EINVAL, "rxg_group_rx_burst_dev: member %u is flow-partitioned (%u of %u); a group "
+                                  "cuts contiguous shards and needs whole tables", i, part, nparts);
+        total += shards[i].n;
+    }
+    if (total > UINT32_MAX) return gfail(-EINVAL, "rxg_group_rx_burst_dev: %llu frames", (unsigned long long)total);
+    g->shard_off.assign(k, 0);
+    g->shard_n.assign(k, 0);
+    uint32_t o = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        g->shard_off[i] = o;
+        g->shard_n[i] = shards[i].n;
+        o += shards[i].n;
+    }
+    g->last_n = o;
+    for (uint32_t i = 0; i < k; ++i) {
+        const int rc = rxg_rx_burst_dev(g->m[i], &shards[i], nullptr);
+        if (rc) return gfail(rc, "member %u: %s", i, rxg_last_error());
+    }
+    g->burst_ok = true;
+    return 0;
+}
+
+extern "C" int rxg_group_sync(rxg_group *g)
+{
+    if (!g) return gfail(-EINVAL, "rxg_group_sync: group NULL");
+    return each(g, [&](rxg_ctx *c) { return rxg_sync(c); });
 }
 
 extern "C" int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, void *const *mbufs,
@@ -320,24 +428,46 @@ static constexpr size_t kCounterWords = (size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS
 
 // One communicator per member over the members' devices; only for distinct GPUs (RCCL
 // takes one rank per device).
+static void free_merged(rxg_group *g)
+{
+    for (size_t i = 0; i < g->merged.size(); ++i)
+        if (g->merged[i]) (void)rxg_dev_free(g->m[i], g->merged[i]);
+    g->merged.clear();
+}
+
 static int rccl_setup(rxg_group *g)
 {
     if (g->rccl >= 0) return 0;
     g->rccl = 0;
     const std::set<int32_t> distinct(g->devices.begin(), g->devices.end());
-    if (distinct.size() != g->devices.size()) return 0;  // members share a GPU: host sum
+    if (distinct.size() != g->devices.size()) {  // members share a GPU: host sum
+        g->rccl_why = "members share a GPU (RCCL takes one rank per device)";
+        return 0;
+    }
+    const Rccl &R = rccl_lib();
+    if (!R.ok) {  // no RCCL on this host: the sum is exact on the host too
+        g->rccl_why = R.why;
+        return 0;
+    }
     const int n = (int)g->m.size();
     g->merged.assign((size_t)n, nullptr);
     for (int i = 0; i < n; ++i)
-        if (rxg_dev_alloc(g->m[(size_t)i], kCounterWords * sizeof(uint64_t), &g->merged[(size_t)i]))
-            return gfail(-ENOMEM, "rxg_group_counters_read: member %d: %s", i, rxg_last_error());
+        if (rxg_dev_alloc(g->m[(size_t)i], kCounterWords * sizeof(uint64_t), &g->merged[(size_t)i])) {
+            const int rc = gfail(-ENOMEM, "rxg_group_counters_read: member %d: %s", i, rxg_last_error());
+            free_merged(g);
+            g->rccl = -1;  // retried at the next read
+            return rc;
+        }
     g->comms.assign((size_t)n, nullptr);
-    const ncclResult_t r = ncclCommInitAll(g->comms.data(), n, g->devices.data());
+    const ncclResult_t r = R.CommInitAll(g->comms.data(), n, g->devices.data());
     if (r != ncclSuccess) {
         g->comms.clear();
-        return gfail(-EIO, "rxg_group_counters_read: ncclCommInitAll: %s", ncclGetErrorString(r));
+        free_merged(g);
+        g->rccl = -1;
+        return gfail(-EIO, "rxg_group_counters_read: ncclCommInitAll: %s", R.GetErrorString(r));
     }
     g->rccl = 1;
+    g->rccl_why.clear();
     return 0;
 }
 
@@ -355,16 +485,17 @@ extern "C" int rxg_group_counters_read(rxg_group *g, uint64_t *out)
         const size_t n = g->m.size();
         for (size_t i = 0; i < n; ++i)  // every burst's counter adds are done (stream order)
             if ((rc = rxg_sync(g->m[i]))) return gfail(rc, "member %zu: %s", i, rxg_last_error());
-        if (ncclGroupStart() != ncclSuccess) return gfail(-EIO, "rxg_group_counters_read: ncclGroupStart");
+        const Rccl &R = rccl_lib();
+        if (R.GroupStart() != ncclSuccess) return gfail(-EIO, "rxg_group_counters_read: ncclGroupStart");
         for (size_t i = 0; i < n; ++i) {
-            const ncclResult_t r = ncclAllReduce(rxg_counters_dev(g->m[i]), g->merged[i], kCounterWords, ncclUint64,
-                                                 ncclSum, g->comms[i], (hipStream_t)rxg_stream(g->m[i]));
+            const ncclResult_t r = R.AllReduce(rxg_counters_dev(g->m[i]), g->merged[i], kCounterWords, ncclUint64,
+                                               ncclSum, g->comms[i], (hipStream_t)rxg_stream(g->m[i]));
             if (r != ncclSuccess) {
-                (void)ncclGroupEnd();
-                return gfail(-EIO, "rxg_group_counters_read: ncclAllReduce: %s", ncclGetErrorString(r));
+                (void)R.GroupEnd();
+                return gfail(-EIO, "rxg_group_counters_read: ncclAllReduce: %s", R.GetErrorString(r));
             }
         }
-        if (ncclGroupEnd() != ncclSuccess) return gfail(-EIO, "rxg_group_counters_read: ncclGroupEnd");
+        if (R.GroupEnd() != ncclSuccess) return gfail(-EIO, "rxg_group_counters_read: ncclGroupEnd");
         std::vector<uint64_t> rows(kCounterWords);
         if ((rc = rxg_memcpy_d2h(g->m[0], rows.data(), g->merged[0], kCounterWords * sizeof(uint64_t), nullptr)) ||
             (rc = rxg_sync(g->m[0])))
@@ -387,6 +518,11 @@ extern "C" int rxg_group_counters_rccl(rxg_group *g)
     if (!g) return gfail(-EINVAL, "rxg_group_counters_rccl: group NULL");
     const int rc = rccl_setup(g);
     return rc ? rc : g->rccl;
+}
+
+extern "C" const char *rxg_group_counters_rccl_why(rxg_group *g)
+{
+    return g ? g->rccl_why.c_str() : "";
 }
 
 extern "C" const char *rxg_group_last_error(void) { return g_err; }

@@ -271,6 +271,9 @@ def load_library(path: str = LIB_PATH):
         "rxg_group_rcv_set": (C.c_int, [vp, i32, u32, u32]),
         "rxg_group_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
         "rxg_group_rx_replay": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, vp, u32, u32]),
+        "rxg_group_rx_burst_dev": (C.c_int, [vp, C.POINTER(DevBatch), u32]),
+        "rxg_group_sync": (C.c_int, [vp]),
+        "rxg_group_counters_rccl_why": (C.c_char_p, [vp]),
         "rxg_group_payload_take": (C.c_int, [vp, i32, u32, u32, C.POINTER(PayloadMsg)]),
         "rxg_group_replaying": (i32, [vp]),
         "rxg_group_counters_reset": (C.c_int, [vp]),
@@ -773,6 +776,16 @@ class Group:
                 "rxg_group_rx_burst")
         return out
 
+    def rx_burst_dev(self, shards, rec_kind: int = REC16):
+        """rxg_group_rx_burst_dev: shards[i] = (frames ptr, off64 ptr, len ptr, n, out ptr) in
+        memory member i reads, member i's contiguous share of the burst in packet order.
+        Asynchronous; sync() waits."""
+        arr = (DevBatch * max(len(shards), 1))(*[DevBatch(f, o, l, n, rec_kind, out) for f, o, l, n, out in shards])
+        _gcheck(_lib.rxg_group_rx_burst_dev(self.g, arr, len(shards)), "rxg_group_rx_burst_dev")
+
+    def sync(self):
+        _gcheck(_lib.rxg_group_sync(self.g), "rxg_group_sync")
+
     def rx_replay(self, ops, mbufs, frames, recs, n: int, stride: int):
         """rxg_group_rx_replay with ctypes arguments (HandoffOps, void* arrays, record pointer)."""
         _gcheck(_lib.rxg_group_rx_replay(self.g, C.byref(ops), mbufs, frames, recs, n, stride),
@@ -800,6 +813,10 @@ class Group:
         rc = _lib.rxg_group_counters_rccl(self.g)
         _gcheck(min(rc, 0), "rxg_group_counters_rccl")
         return rc == 1
+
+    def counters_rccl_why(self) -> str:
+        """Why the merge runs on the host ('' when it is RCCL)."""
+        return _lib.rxg_group_counters_rccl_why(self.g).decode(errors="replace")
 
 
 def synthetic_tcb_table(nflows: int, dst_raw: int = None, dport: int = 80):

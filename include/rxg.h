@@ -590,8 +590,10 @@ const char *rxg_last_error(void);
 /*    mirrors: the rxg_group_* mirror calls apply to all of them;             */
 /*  - rxg_group_rx_burst cuts the burst into one contiguous shard per member   */
 /*    (ceil(n/ndev) frames, so cfg->max_batch is per shard), runs the shards   */
-/*    concurrently (one host thread per member) and returns the records in     */
-/*    packet order;                                                            */
+/*    concurrently (one worker thread per member, kept for the group's life)   */
+/*    and returns the records in packet order;                                 */
+/*  - rxg_group_rx_burst_dev takes a burst already in GPU-visible memory as    */
+/*    one shard per member and launches every member at once (no host copy);   */
 /*  - rxg_group_rx_replay replays the shards in packet order.  Handlers mirror */
 /*    their tcbs[] writes with rxg_group_tcb_* (not the member calls), so a    */
 /*    later member's replay sees them and re-classifies what they affect: the  */
@@ -621,6 +623,21 @@ int rxg_group_arp_disable(rxg_group *g);
 int rxg_group_rcv_set(rxg_group *g, int32_t idx, uint32_t cur_seq, uint32_t pairs_pending);
 int rxg_group_rx_burst(rxg_group *g, const rxg_pkt_view *pkts, uint32_t n, uint32_t rec_kind,
                        void *out_host);
+/* Device-resident group burst (contiguous batches to the GPUs, the host
+   replays in global packet order), replacing main.c:391-399's loop for frames the caller
+   already has in GPU-visible memory.  shards[i] (nshards = group size) is member i's
+   contiguous share of the burst, in packet order (shard 0 first; any n, 0 included), with
+   the rxg_dev_batch rules of rxg_rx_burst_dev in memory member i's GPU reads: its HBM, or
+   host memory registered on member i (rxg_host_register; e.g. the mbuf pool registered on
+   every member).  Every shard has the same rec_kind.  Each member classifies its shard
+   against its replica of the mirror as it stands at the call; the launches are asynchronous,
+   one per member on its own stream, so the shards run concurrently.  rxg_group_sync waits
+   for them; rxg_group_rx_replay then replays n = sum of the shards' n records, laid out in
+   packet order with that stride, exactly as after rxg_group_rx_burst (each member's shard
+   buffers must stay valid until the replay returns). */
+int rxg_group_rx_burst_dev(rxg_group *g, const rxg_dev_batch *shards, uint32_t nshards);
+/* Waits for every member's stream (rxg_sync on each). */
+int rxg_group_sync(rxg_group *g);
 int rxg_group_rx_replay(rxg_group *g, const rxg_handoff_ops *ops, void *const *mbufs,
                         void *const *frames, const void *recs, uint32_t n, uint32_t rec_stride);
 /* rxg_payload_take on the member whose shard is being replayed (0 outside a replay);
@@ -633,8 +650,12 @@ int rxg_group_counters_reset(rxg_group *g);
    blocks over xGMI when the members are distinct GPUs (one communicator per member,
    ncclCommInitAll at the first call), else summed on the host (members sharing a GPU). */
 int rxg_group_counters_read(rxg_group *g, uint64_t *out);
-/* 1 when rxg_group_counters_read merges with RCCL, 0 when on the host; negative on error. */
+/* 1 when rxg_group_counters_read merges with RCCL, 0 when on the host; negative on error.
+   RCCL is loaded at the first merge over distinct GPUs (dlopen of librccl.so): librxg.so
+   does not depend on it, and a host without it merges on the host (same sums). */
 int rxg_group_counters_rccl(rxg_group *g);
+/* Why the merge is on the host (empty when RCCL is used or not decided yet). */
+const char *rxg_group_counters_rccl_why(rxg_group *g);
 /* Last error of a group call on this thread (member errors carry their text). */
 const char *rxg_group_last_error(void);
 

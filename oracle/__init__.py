@@ -45,7 +45,7 @@ def lib(opt: str = "O2") -> C.CDLL:
     vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int32
     L.orc_calculate_checksum.restype = C.c_uint16
     L.orc_calculate_checksum.argtypes = [vp, C.c_int]
-    for fn in (L.orc_rx_batch, L.orc_rx_batch_faithful):
+    for fn in (L.orc_rx_batch, L.orc_rx_batch_faithful, L.orc_rx_batch_shipped):
         fn.restype = C.c_int
         fn.argtypes = [vp, vp, vp, u32, vp, vp, i32, vp, vp]
     L.orc_tx_cksum_batch.restype = C.c_int
@@ -66,8 +66,9 @@ def calculate_checksum(data: bytes) -> int:
     return lib().orc_calculate_checksum(buf, len(data))
 
 
-def rx_batch(arena, off64, lens, tcbs, live=None, faithful=False, opt="O2"):
-    """Records (REC48_DTYPE) and counters (u64[16]) for a packed batch."""
+def rx_batch(arena, off64, lens, tcbs, live=None, faithful=False, opt="O2", shipped=False):
+    """Records (REC48_DTYPE) and counters (u64[16]) for a packed batch.  shipped (timing only,
+    with faithful): the reference as shipped, without the rx checksum verify."""
     n = len(lens)
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     off64 = np.ascontiguousarray(off64, dtype=np.uint32)
@@ -77,7 +78,8 @@ def rx_batch(arena, off64, lens, tcbs, live=None, faithful=False, opt="O2"):
             else np.ascontiguousarray(live, dtype=np.uint8))
     out = np.zeros(n, dtype=REC48_DTYPE)
     cnt = np.zeros(NCOUNTERS, dtype=np.uint64)
-    fn = lib(opt).orc_rx_batch_faithful if faithful else lib(opt).orc_rx_batch
+    fn = (lib(opt).orc_rx_batch_shipped if shipped else lib(opt).orc_rx_batch_faithful) if faithful \
+        else lib(opt).orc_rx_batch
     fn(_p(arena), _p(off64), _p(lens), n, _p(tcbs) if len(tcbs) else None,
        _p(live) if len(live) else None, len(tcbs), _p(out), _p(cnt))
     return out, cnt

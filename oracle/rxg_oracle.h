@@ -49,6 +49,11 @@ int orc_rx_batch(const uint8_t *arena, const uint32_t *off64, const uint16_t *le
 int orc_rx_batch_faithful(const uint8_t *arena, const uint32_t *off64, const uint16_t *len,
                           uint32_t n, const rxg_tcb_tuple *tcbs, const uint8_t *live,
                           int32_t ntcb, rxg_rec48 *out, uint64_t *counters);
+/* Timing only: orc_rx_batch_faithful without the rx checksums, i.e. the reference as shipped
+   (tcp_in.c:37's verify compiled out); checksum fields and ok flags are left 0. */
+int orc_rx_batch_shipped(const uint8_t *arena, const uint32_t *off64, const uint16_t *len,
+                         uint32_t n, const rxg_tcb_tuple *tcbs, const uint8_t *live,
+                         int32_t ntcb, rxg_rec48 *out, uint64_t *counters);
 void orc_arp_reset(void);
 int orc_arp_count(void);
 

@@ -125,6 +125,15 @@ def test_product_does_not_link_the_oracle():
     assert "orc_" not in syms
 
 
+def test_product_does_not_need_rccl_at_load():
+    """RCCL serves only the group's counter merge over distinct GPUs; it is
+    dlopen'ed there, so single-GPU users and the plain-C rx loop load librxg.so without it."""
+    out = subprocess.run(["readelf", "-d", rxg.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    needed = [line for line in out.splitlines() if "(NEEDED)" in line]
+    assert needed and not any("rccl" in line for line in needed), needed
+
+
 def test_pack_arena_layout():
     frames = [b"a" * 10, b"b" * 64, b"c" * 65, b""]
     arena, off, lens = rxg.pack_arena(frames)

@@ -42,3 +42,31 @@ def test_misaligned_buffers_are_refused(engine):
     finally:
         for d in (da, do, dl, dout):
             d.free()
+
+
+def test_replay_refused_after_a_rejected_launch(engine):
+    """a launch refused at validation (misaligned records) leaves nothing to
+    replay; a replay whose n matches the previous, good burst is refused, not replayed from
+    that burst's records."""
+    frames = [pktgen.frame(sport=5000 + i) for i in range(64)]
+    arena, off, lens = pktgen.pack_arena(frames)
+    lib = rxg.load_library()
+    da, do, dl = engine.to_device(arena), engine.to_device(off), engine.to_device(lens)
+    dout = engine.alloc(len(frames) * 16 + 64)
+    try:
+        n = len(frames)
+        good = rxg.DevBatch(da.ptr, do.ptr, dl.ptr, n, rxg.REC16, dout.ptr)
+        assert lib.rxg_rx_burst_dev(engine.ctx, C.byref(good), None) == 0
+        engine.sync()
+        recs = dout.download(rxg.REC16_DTYPE, n)
+        ops = rxg.HandoffOps()
+        bufs = [C.create_string_buffer(f, 64) for f in frames]
+        ptrs = (C.c_void_p * n)(*[C.addressof(b) for b in bufs])
+        assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, n, 16) == 0
+        bad = rxg.DevBatch(da.ptr, do.ptr, dl.ptr, n, rxg.REC16, dout.ptr + 8)
+        assert lib.rxg_rx_burst_dev(engine.ctx, C.byref(bad), None) == -22
+        assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, n, 16) == -22
+        assert b"failed" in lib.rxg_last_error()
+    finally:
+        for d in (da, do, dl, dout):
+            d.free()

@@ -184,6 +184,7 @@ def test_group_counter_merge_rccl():
     for devs, rccl in ((list(range(torch.cuda.device_count())), True), ([0, 0], False)):
         with rxg.Group(devs, **MB) as g:
             assert g.counters_rccl() == rccl
+            assert (g.counters_rccl_why() == "") == rccl, g.counters_rccl_why()
             g.tcb_load(tcb, live)
             g.counters_reset()
             g.rx_burst(frames, rxg.REC16)
@@ -191,3 +192,73 @@ def test_group_counter_merge_rccl():
             assert g.counters().tolist() == ecnt.tolist()
             g.rx_burst(frames, rxg.REC16)
             assert g.counters().tolist() == (2 * ecnt).tolist()
+
+
+def _dev_shards(g, frames, cuts, kind):
+    """Member i's share frames[cuts[i]:cuts[i+1]] packed into member i's device memory."""
+    shards, keep = [], []
+    for i, m in enumerate(g.members):
+        part = frames[cuts[i]:cuts[i + 1]]
+        arena, off, lens = pktgen.pack_arena(part) if part else pktgen.pack_arena([pktgen.frame()])
+        da, do, dl = m.to_device(arena), m.to_device(off), m.to_device(lens)
+        dout = m.alloc(max(len(part), 1) * kind)
+        keep.append((m, da, do, dl, dout, len(part)))
+        shards.append((da.ptr, do.ptr, dl.ptr, len(part), dout.ptr))
+    return shards, keep
+
+
+@pytest.mark.parametrize("ndev,seed,kind", [(2, 11, rxg.REC16), (3, 12, rxg.REC8), (3, 13, rxg.REC16)])
+def test_group_dev_burst_replay_sequential_equivalence(ndev, seed, kind):
+    """rxg_group_rx_burst_dev: each member's contiguous share already in its GPU's memory
+    (uneven shares, one empty), every member launched at once; the records equal the host
+    group burst's, and burst + replay in global packet order equals the reference's
+    sequential ether_in loop under in-burst SYN / FIN / remove writes (main.c:391-399)."""
+    rng = random.Random(seed)
+    rows, frames = scenario(seed)
+    exp, ecnt, erows = sequential_reference(rows, frames)
+    tcb, live = pktgen.table_arrays(rows)
+    n = len(frames)
+    cuts = [0] + sorted(rng.sample(range(1, n), ndev - 1)) + [n]
+    if ndev == 3:
+        cuts[2] = cuts[1]  # member 1 gets nothing
+    with rxg.Group([0] * ndev, **MB) as g:
+        g.tcb_load(tcb, live)
+        want = g.rx_burst(frames, kind)  # the host-buffer group burst, same table
+        g.counters_reset()
+        shards, keep = _dev_shards(g, frames, cuts, kind)
+        try:
+            g.rx_burst_dev(shards, kind)
+            g.sync()
+            recs = np.concatenate([dout.download(rxg.rec_dtype(kind), k) for (_, _, _, _, dout, k) in keep])
+            assert recs.tobytes() == want.tobytes()
+            model = Model(rows, g)
+            bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
+            got = [None] * n
+            ops = _ops(frames, bufs, got, model)
+            ptrs = (C.c_void_p * n)(*[C.addressof(b) for b in bufs])
+            g.rx_replay(ops, ptrs, ptrs, recs.ctypes.data, n, kind)
+        finally:
+            for (m, *bufs_) in keep:
+                for d in bufs_[:4]:
+                    d.free()
+    for i, (v, idx, st) in enumerate(exp):
+        if v == rxg.V_DISPATCH:
+            assert got[i] == ("switch", idx, st), (i, got[i], exp[i])
+        elif v in (rxg.V_RST_NOPCB, rxg.V_RST_LISTEN_NONSYN):
+            assert got[i] == ("rst",), (i, got[i], exp[i])
+    assert model.rows == erows
+
+
+def test_group_dev_burst_arguments():
+    with rxg.Group([0, 0], **MB) as g:
+        with pytest.raises(rxg.RxgError, match="1 shards for 2 members"):
+            g.rx_burst_dev([(0, 0, 0, 0, 0)], rxg.REC16)
+        arr = (rxg.DevBatch * 2)(rxg.DevBatch(0, 0, 0, 0, rxg.REC16, 0), rxg.DevBatch(0, 0, 0, 0, rxg.REC8, 0))
+        assert rxg.load_library().rxg_group_rx_burst_dev(g.g, arr, 2) == -22
+        assert b"rec_kind" in rxg.load_library().rxg_group_last_error()
+        # a failed group burst leaves nothing to replay
+        ops = rxg.HandoffOps()
+        ptrs = (C.c_void_p * 1)()
+        recs = np.zeros(1, dtype=rxg.REC16_DTYPE)
+        with pytest.raises(rxg.RxgError, match="last group burst failed"):
+            g.rx_replay(ops, ptrs, ptrs, recs.ctypes.data, 0, 16)

@@ -152,3 +152,43 @@ def test_mirror_write_between_bursts_on_caller_streams(engine, second):
         for v in dev.values():
             if isinstance(v, rxg.DevArray):
                 v.free()
+
+
+def test_mirror_write_waits_for_every_reader_stream(engine):
+    """a long burst on s1, then a short one on s2, then removals, then a burst on
+    the context's stream, with no host synchronisation in between.  The removals must wait
+    for BOTH readers (one event per reader stream, csrc/rxg_host.cpp order_table_reader_after):
+    the s1 burst classifies every frame against the old table."""
+    n, nflows, m = 1 << 20, 1000, 4096
+    dev = engine.synth(n=n, nflows=nflows, len_a=1500, seed=78, with_flows=True)
+    t0, l0 = rxg.synthetic_tcb_table(nflows)
+    flows = dev["flow"].download(np.uint32, n)
+    out_a, out_s, out_c = engine.alloc(n * 16), engine.alloc(m * 16), engine.alloc(n * 16)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        for _ in range(3):
+            engine.tcb_load(t0, l0)
+            engine.tcb_sync()
+            engine.sync()
+            torch.cuda.synchronize()
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out_a.ptr, 16, s1.cuda_stream)
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, m, out_s.ptr, 16, s2.cuda_stream)
+            for i in range(1, nflows + 1, 2):   # flows 0, 2, 4, ... lose their TCB
+                engine.tcb_remove(i)
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out_c.ptr, 16, None)
+            torch.cuda.synchronize()
+            engine.sync()
+            a = out_a.download(rxg.REC16_DTYPE, n)
+            s = out_s.download(rxg.REC16_DTYPE, m)
+            c = out_c.download(rxg.REC16_DTYPE, n)
+            assert (a["tcb_idx"] == flows.astype(np.int32) + 1).all(), "the s1 burst saw the removals"
+            assert (s["tcb_idx"] == flows[:m].astype(np.int32) + 1).all()
+            gone = (flows % 2) == 0
+            assert (c["tcb_idx"][~gone] == flows[~gone].astype(np.int32) + 1).all()
+            assert (c["tcb_idx"][gone] == 0).all() and (c["verdict"][gone] == rxg.V_RST_LISTEN_NONSYN).all()
+    finally:
+        for d in (out_a, out_s, out_c):
+            d.free()
+        for v in dev.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()

@@ -194,3 +194,21 @@ def test_golden_tx_regression():
     arena[pos[inside]] = 0
     out = oracle.tx_batch(arena, off, lens)
     assert np.array_equal(out[pos], t["cksum_bytes"])
+
+
+def test_shipped_mode_classifies_as_faithful():
+    """orc_rx_batch_shipped (timing only: the reference as shipped, tcp_in.c:37's verify
+    compiled out) gives the faithful path's classification, with no checksum fields."""
+    rows, frames = pktgen.parity_set(seed=7, n=800)
+    arena, off, lens = pktgen.pack_arena(frames)
+    tcb, live = pktgen.table_arrays(rows)
+    oracle.arp_reset()
+    a, ca = oracle.rx_batch(arena, off, lens, tcb, live, faithful=True)
+    oracle.arp_reset()
+    b, cb = oracle.rx_batch(arena, off, lens, tcb, live, faithful=True, shipped=True)
+    oracle.arp_reset()
+    for k in ("tcb_idx", "verdict", "state", "datalen", "tcp_flags"):
+        assert (a["c"][k] == b["c"][k]).all(), k
+    assert not b["c"]["ip_cksum"].any() and not b["c"]["tcp_cksum"].any()
+    ok = 0x01 | 0x02  # RXG_F_IP_OK | RXG_F_TCP_OK
+    assert ((a["c"]["flags"] & np.uint8(0xFF ^ ok)) == b["c"]["flags"]).all()
