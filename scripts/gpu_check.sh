@@ -1,11 +1,23 @@
 #!/bin/bash
-# GPU-box checks: parity tests, smoke, the default bench, a rocprofv3 kernel-trace summary
-# of the bench's C3 workload and two PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic.
-# Every GPU step has its own time limit; a fault/abort/timeout ends the script there.
-# Usage: scripts/gpu_check.sh [tag] [steps...]   (steps default: all)
+# The one GPU-box driver: each step its own time limit; a fault / abort / timeout (any exit
+# other than pass, test failures or no tests) ends the script there, nothing more runs.
+#
+# Usage: scripts/gpu_check.sh TAG STEP...       (outputs under gpurun_out/TAG/)
+#   pytest      the whole -m gpu suite
+#   smoke       __graft_entry__.smoke()
+#   bench       the default bench line (bench.json)
+#   rehearse    bench.py with 2 ranks on the box's one GPU (gloo collectives; a rehearsal,
+#               never a scaling figure)
+#   prof        rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes per workload
+#               (scripts/gpu_prof.sh; PROF_WLS, default "c3 c4 c2 c2multi"; REC, default 8)
+#   sq          SQ counter passes per workload (scripts/gpu_sq.sh; SQ_WLS)
+#   ab          in-process kernel A/B, records checked (scripts/gpu_ab.sh; VARIANTS, WLS comma-separated)
+#   crossover   small-burst crossover against the reference CPU path (scripts/crossover.py)
+#   group       group-burst latency (scripts/grouplat.py)
+#   churn       burst + replay under SYN/FIN churn (scripts/churnbench.sh)
+#   pg          payload-gather A/B (scripts/pgbench.py; PG_VARIANTS)
 set -u
-TAG=${1:-r01}; shift || true
-STEPS=${*:-"pytest smoke bench prof pmc pgprof"}
+TAG=${1:?usage: gpu_check.sh TAG STEP...}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -16,21 +28,27 @@ step() {  # step <name> <seconds> <cmd...>
   local rc=$?
   echo "rc=$rc"; grep -v "amdgpu.ids" "$OUT/$name.log" | tail -n 12
   case $rc in
-    0|1|5) return 0 ;;            # pass / test failures / no tests: GPU still healthy
+    0) return 0 ;;
+    1|5) [ "$name" = pytest_gpu ] && { echo "STOP: tests failed"; exit 1; }; return 0 ;;
     *) echo "STOP: $name exited $rc"; exit $rc ;;
   esac
 }
-has() { [[ " $STEPS " == *" $1 "* ]]; }
-BENCH_PROF="python3 bench.py --steps 20 --warmup 5 --no-cpu --no-legs"
 rocm-smi --showproductname > "$OUT/rocm-smi.log" 2>&1 || true
-has pytest && step pytest_gpu 600 python -m pytest tests -m gpu -x -q
-has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-has bench && step bench 400 python bench.py
-has prof && step rocprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- $BENCH_PROF
-has pmc && step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rx_kernel -d "$OUT/pmc_fetch" -o run --output-format csv -- $BENCH_PROF
-has pmc && step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rx_kernel -d "$OUT/pmc_write" -o run --output-format csv -- $BENCH_PROF
-PG="python3 scripts/pgbench.py --workloads c3 --iters 10"
-has pgprof && step pg_rocprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/pg_prof" -o run --output-format csv -- $PG
-has pgprof && step pg_pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex pg_gather -d "$OUT/pg_pmc_fetch" -o run --output-format csv -- $PG
-has pgprof && step pg_pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex pg_gather -d "$OUT/pg_pmc_write" -o run --output-format csv -- $PG
+for S in "$@"; do
+  case $S in
+    pytest)    step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    smoke)     step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)     step bench 500 python -u bench.py; cp "$OUT/bench.log" "$OUT/bench.json" ;;
+    rehearse)  step rehearse2 600 env RXG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
+                 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 3 ;;
+    prof)      step prof 900 env REC=${REC:-8} bash scripts/gpu_prof.sh "$TAG/prof" ${PROF_WLS:-c3 c4 c2 c2multi} ;;
+    sq)        step sq 600 env REC=${REC:-8} bash scripts/gpu_sq.sh ${SQ_WLS:-c4 c3} ;;
+    ab)        step ab 800 env TAG="$TAG/ab" bash scripts/gpu_ab.sh ;;
+    crossover) step crossover 500 python3 -u scripts/crossover.py ;;
+    group)     step grouplat 200 python3 -u scripts/grouplat.py ;;
+    churn)     step churn 600 bash scripts/churnbench.sh "$OUT/churn.jsonl" ;;
+    pg)        step pg 500 env TAG="$TAG/pg" VARIANTS=${PG_VARIANTS:-0} bash scripts/gpu_pg.sh ;;
+    *) echo "unknown step $S"; exit 2 ;;
+  esac
+done
 echo "=== done"
