@@ -140,6 +140,8 @@ __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__bui
 // were not built: a returning device-scope atomicAdd on one word saturates at ≈88 claims/µs
 // (MI355X_MICROARCH.md, dequeue), ten times fewer than the 64 B burst's ≈860 slices/µs.
 constexpr uint32_t kMaxPieces = 4;
+// launches with at least this many slices per wave take the two-deep all-small pipeline
+constexpr uint32_t kDeepSlicesPerWave = 16;
 
 template <bool MULTI>
 struct BurstCursor {
@@ -976,11 +978,15 @@ struct ProbeLoads {
     uint32_t hb;           // this lane's frame's first bucket
 };
 
+template <int STRIP = 0>
 __device__ __forceinline__ ProbeLoads probe_issue_coalesced(const RxArgs &a, const Fields &F, int lane)
 {
     static_assert(kSlotsPerBucket == 4, "one bucket = four 16-byte slots = four lanes");
     ProbeLoads L;
     L.hb = probe_bucket(a, F);
+    // STRIP 2097152 (experiment, timing only): every probe reads one of the first 256 buckets
+    // (16 KiB, cache-resident): the probe's instructions without its memory traffic
+    if constexpr ((STRIP & 2097152) != 0) L.hb &= 255u;
     const uint4 *bk = a.t.buckets + (lane & 3);
     const uint32_t h0 = lane_read(L.hb, (lane >> 2)), h1 = lane_read(L.hb, 16 + (lane >> 2));
     const uint32_t h2 = lane_read(L.hb, 32 + (lane >> 2)), h3 = lane_read(L.hb, 48 + (lane >> 2));
@@ -1025,7 +1031,7 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, uint32_t f, bool
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
     if constexpr ((STRIP & 4096) == 0 && (STRIP & 2) == 0) {
         const int lane = (int)(threadIdx.x & 63);
-        const Probe P = cached ? probe_none() : probe_transpose(probe_issue_coalesced(a, F, lane), lane, tsf);
+        const Probe P = cached ? probe_none() : probe_transpose(probe_issue_coalesced<STRIP>(a, F, lane), lane, tsf);
         classify_finish<MODE, STRIP>(a, f, valid, len, F, P, wc, pr, fc, cached);
     } else {
         (void)tsf;
@@ -1176,6 +1182,62 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
             nslot = (fc.meta >> 9) & 1u;
             arp_learn = (fc.meta >> 10) & 1u;
         }
+    } else if (is_tcp && !(STRIP & 2) && (STRIP & 4194304)) {
+        // experiment, timing only: the first bucket's first slot is taken as the hit (no
+        // compare loop, no second bucket): the probe's loads and transpose without its search
+        idx = (int32_t)(P.s[0].w & kIdxMask);
+        st = P.s[0].w >> kStateShift;
+        fc.ports = ports;
+        fc.dst = dst_raw;
+        fc.src = src_host;
+        fc.idx = idx;
+        fc.meta = st | kFcValid;
+    } else if (is_tcp && !(STRIP & 2) && (STRIP & 8388608)) {
+        // experiment STRIP 8388608: the first bucket (already loaded and transposed) compared
+        // straight-line by every lane; only lanes whose tuple may sit in a later bucket (first
+        // bucket full, no match: ≈0.4 % of the lanes at 64 K flows) run the linear probe, under
+        // a wave-uniform test
+        uint32_t v = kEmpty;
+        bool empty = false;
+#pragma unroll
+        for (int k = 0; k < kSlotsPerBucket; ++k) {
+            const bool m = P.s[k].x == ports && P.s[k].y == dst_raw && P.s[k].z == src_host;
+            v = m ? P.s[k].w : v;  // a free slot holds kEmpty: a match there is no hit
+            empty |= P.s[k].w == kEmpty;
+        }
+        const bool more = v == kEmpty && !empty;
+        if (__ballot(more) != 0ull) {
+            if (more) {
+                uint32_t hb = P.hb;
+                for (uint32_t probe = 1; probe <= a.t.bucket_mask; ++probe) {
+                    hb = (hb + 1u) & a.t.bucket_mask;
+                    const uint4 *b = a.t.buckets + (size_t)hb * kSlotsPerBucket;
+                    bool e2 = false;
+#pragma unroll
+                    for (int k = 0; k < kSlotsPerBucket; ++k) {
+                        const uint4 q = b[k];
+                        if (q.x == ports && q.y == dst_raw && q.z == src_host && q.w != kEmpty) v = q.w;
+                        e2 |= q.w == kEmpty;
+                    }
+                    if (v != kEmpty || e2) break;
+                }
+            }
+        }
+        if (v != kEmpty) {
+            idx = (int32_t)(v & kIdxMask);
+            st = v >> kStateShift;
+        } else {  // pass 2: first LISTENING slot on dport (its state is LISTENING)
+            const int32_t L = a.t.listen[dport];
+            idx = L;
+            lhit = L >= 0;
+            nslot = a.t.min_null < (L >= 0 ? L : a.t.ntcb);
+            if (lhit) st = RXG_LISTENING;
+        }
+        fc.ports = ports;
+        fc.dst = dst_raw;
+        fc.src = src_host;
+        fc.idx = idx;
+        fc.meta = st | ((uint32_t)lhit << 8) | ((uint32_t)nslot << 9) | ((uint32_t)arp_learn << 10) | kFcValid;
     } else if (is_tcp && !(STRIP & 2)) {
         uint32_t hb = P.hb;
         uint4 sl[kSlotsPerBucket];
@@ -1505,10 +1567,54 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     return nxt;
 }
 
+// Two-deep form (experiment STRIP 16777216): frames of two slices in flight with the same two
+// register buffers.  A buffer is free once its slice has been transposed into LDS, so right
+// after the transpose of slice s (vb[P]) the frames of slice s + 2 nwaves are issued into
+// vb[P], while vb[1-P] still holds s + nwaves (issued one step earlier).  Descriptors run
+// three slices ahead and are issued before the frames (vmcnt retires in order: the next
+// step's check of them then waits for nothing younger).  pend: s + nwaves's frames are in
+// vb[1-P]; returns whether the run continues with it.
+template <int P, int MODE, int STRIP, bool SEL, int RS, typename BC>
+__device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t &s, uint32_t nslices,
+                                            uint32_t nwaves, uint32_t &c_off, uint32_t &c_len, uint32_t &n_off,
+                                            uint32_t &n_len, uint32_t &y_off, uint32_t &y_len, bool &pend,
+                                            uint4 (&vb)[2][4], RecRing<MODE, RS> &ring, WaveCounters &wc, Rec &rec,
+                                            FlowCache &fc, unsigned long long &bytes, BC &bc)
+{
+    const uint32_t s1 = s + nwaves, s2 = s + 2u * nwaves;
+    uint32_t d[4][4];
+    uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
+    transpose_small_slice(vb[P], lane, sf, d);
+    const Fields F = fields_small<MODE>(nullptr, c_len, d);
+    const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
+    const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
+    const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
+    const Probe PO = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, true, F);
+    uint32_t z_off, z_len;
+    load_desc<SEL, std::remove_reference_t<decltype(bc)>>(a, s + 3u * nwaves, lane, z_off, z_len, bc);
+    const bool nxt2 = pend && s2 < nslices && slice_frames(a, uniform(s2), bc) == 64u && __ballot(y_len <= 64u) == ~0ull;
+    if (nxt2) issue_small_slice<true>(a, y_off, y_len, lane, vb[P]);
+    classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PO, wc, rec, fc, cached);
+    bytes += c_len;
+    if (!(STRIP & 4)) {
+        if (ring.n == RS) ring.template flush<true>(a, lane, bc);
+        ring.put(s, lane, rec);
+    }
+    const bool cont = pend;
+    pend = nxt2;
+    s = s1;
+    c_off = n_off; c_len = n_len;
+    n_off = y_off; n_len = y_len;
+    y_off = z_off; y_len = z_len;
+    return cont;
+}
+
 template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
-          bool DEFER = false, bool DTOP = true, int WPE = 0>
+          bool DEFER = false, bool DTOP = true, int WPE = 0, bool DEEP = false>
 // WPE 0: no bound, except 3 waves per SIMD (at most 168 VGPRs) for rx kernels with the
-// software-pipelined rounds (experiment STRIP 32768), which would otherwise take 170 and drop to 2
+// software-pipelined rounds (experiment STRIP 32768), which would otherwise take 170 and drop to 2.
+// DEEP: runs of all-small slices prefetched two slices deep (small_step2); launch_rx picks it
+// for launches of at least kDeepSlicesPerWave slices per wave.
 __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx_kernel(RxArgs a)
 {
     static_assert(!DEFER || MODE == 8 || MODE == 16, "deferred phase B: REC8 / REC16 only");
@@ -1591,6 +1697,23 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
                 finish_pending();
                 uint4 vb[2][4];
                 issue_small_slice<true>(a, c_off, c_len, lane, vb[0]);
+                if constexpr (DEEP || (STRIP & 16777216) != 0) {
+                    // two-deep (experiment): s + nwaves's frames too when that slice is all-small
+                    const uint32_t s1 = s + nwaves;
+                    bool pend = s1 < nslices && slice_frames(a, uniform(s1), bc) == 64u && __ballot(n_len <= 64u) == ~0ull;
+                    uint32_t y_off, y_len;
+                    load_desc<SEL, std::remove_reference_t<decltype(bc)>>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
+                    if (pend) issue_small_slice<true>(a, n_off, n_len, lane, vb[1]);
+                    for (;;) {
+                        if (!small_step2<0, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off, n_len,
+                                                                  y_off, y_len, pend, vb, ring, wc, rec, fcache, bytes, bc))
+                            break;
+                        if (!small_step2<1, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off, n_len,
+                                                                  y_off, y_len, pend, vb, ring, wc, rec, fcache, bytes, bc))
+                            break;
+                    }
+                    continue;
+                }
                 for (;;) {
                     if (!small_step<0, MODE, STRIP, SEL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
                                                              n_len, vb, ring, wc, rec, fcache, bytes, bc))
@@ -1859,6 +1982,9 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     if (nslices == 0) return hipSuccess;
     uint32_t blocks = (nslices + 3u) / 4u;
     if (blocks > L.max_blocks) blocks = L.max_blocks;
+    // long launches (C2 as 16 bursts: 85 slices per wave) prefetch all-small runs two slices
+    // deep; short ones (one 2^20-frame burst: 5.3 per wave) measured slower with it (§5)
+    const bool deep = nslices >= kDeepSlicesPerWave * blocks * 4u;
     // production kernels use non-temporal loads for the >256 B classes (measured +5 %
     // at 1500 B, -4 % at 64 B: classes 0-2 always use plain loads)
     if (L.sel) {  // re-classification of selected frames (rxg_rx_replay), records of 16 B
@@ -1908,13 +2034,21 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         // 52: the last generation's slices cut into pieces
         case 52: hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a); break;
         default:
-            if (a.nbursts > 1)
+            if (deep && a.nbursts > 1)
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true, false, true, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+            else if (deep)
+                hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, false, true, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+            else if (a.nbursts > 1)
                 hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
             else
                 hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
         }
 #else
-        if (a.nbursts > 1)
+        if (deep && a.nbursts > 1)
+            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true, false, true, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+        else if (deep)
+            hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, false, false, true, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+        else if (a.nbursts > 1)
             hipLaunchKernelGGL((rx_kernel<16, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<16, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
@@ -1952,6 +2086,44 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
                 hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
+        if (L.variant == 67) {  // one-deep all-small pipeline whatever the launch length (round 2)
+            if (a.nbursts > 1)
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 66) {  // all-small runs prefetched two slices deep
+            if (a.nbursts > 1)
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 16777216, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 16777216>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 65 && a.nbursts == 1) {  // per-lane bucket loads + straight-line first bucket
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 4096 | 8388608>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 64 && a.nbursts == 1) {  // first bucket compared straight-line
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 8388608>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 60 && a.nbursts == 1) {  // timing only: cache-resident buckets, no search
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 2097152 | 4194304>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 61 && a.nbursts == 1) {  // timing only: real bucket loads, no search
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 4194304>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 62 && a.nbursts == 1) {  // timing only: cache-resident buckets, real search
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 2097152>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 63 && a.nbursts == 1) {  // timing only: no TCB probe (STRIP 2)
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 2>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
         if (L.variant == 51 && a.nbursts == 1) {  // non-temporal descriptor loads
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 524288>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
@@ -1984,7 +2156,11 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             return hipGetLastError();
         }
 #endif
-        if (a.nbursts > 1)
+        if (deep && a.nbursts > 1)
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, true, false, true, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+        else if (deep)
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, false, false, true, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+        else if (a.nbursts > 1)
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 0, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<8, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);

@@ -138,3 +138,43 @@ def test_small_bursts_pieces(n):
         cnt = eng.counters()
     assert got.tobytes() == exp.tobytes()
     assert cnt.tolist() == ecnt.tolist()
+
+
+@pytest.mark.parametrize("kind", [rxg.REC8, rxg.REC16])
+def test_deep_pipeline_multi_burst(kind):
+    """A launch with >= 16 slices per wave (rxg_kernels.hip kDeepSlicesPerWave) runs the
+    two-deep all-small pipeline: one workgroup (4 waves) over ~150 slices in 7 bursts, runs of
+    64 B slices between mixed ones, bit-exact with the oracle."""
+    rng = random.Random(77)
+    rows, frames = pktgen.parity_set(seed=4343, n=64 * 143 + 37)
+    # long runs of <= 64 B frames so all-small runs of several slices occur per wave
+    for start in (0, 2048, 5000):
+        for i in range(start, start + 1500):
+            src, sport, dport = rng.choice([(0x0A000001, 1024, 80), (0x0A000002, 1025, 80)])
+            frames[i] = pktgen.frame(src_ip=src, sport=sport, dport=dport, payload=bytes(rng.randrange(0, 11)))
+    n = len(frames)
+    cuts = [0] + sorted(rng.sample(range(1, n), 6)) + [n]
+    arena, off, lens, tcb, live, exp, ecnt = _expect(rows, frames, kind)
+    with rxg.Engine(device=0, max_batch=1 << 15, max_bytes=32 << 20, max_blocks=1) as eng:
+        eng.tcb_load(tcb, live)
+        d_arena = eng.to_device(arena)
+        dev, bursts = [], []
+        try:
+            for j in range(len(cuts) - 1):
+                a, b = cuts[j], cuts[j + 1]
+                do, dl, dout = eng.to_device(off[a:b]), eng.to_device(lens[a:b]), eng.alloc((b - a) * kind)
+                dev += [do, dl, dout]
+                bursts.append((do.ptr, dl.ptr, b - a, dout.ptr))
+            eng.counters_reset()
+            eng.rx_bursts_dev(d_arena.ptr, bursts, kind)
+            eng.sync()
+            cnt = eng.counters()
+            got = np.concatenate([dev[3 * j + 2].download(rxg.rec_dtype(kind), cuts[j + 1] - cuts[j])
+                                  for j in range(len(cuts) - 1)])
+            single = eng.rx_arena(arena, off, lens, kind)  # one burst: also >= 16 slices per wave
+        finally:
+            for d in dev + [d_arena]:
+                d.free()
+    assert got.tobytes() == exp.tobytes()
+    assert single.tobytes() == exp.tobytes()
+    assert cnt.tolist() == ecnt.tolist()
