@@ -38,10 +38,10 @@ TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.jso
                  ("c2_64B_1flow", 1 << 20, 16): "profiles/r02/c2/traffic.json",
                  ("c4_imix_64Kflows", 1 << 20, 16): "profiles/r02/c4/traffic.json",
                  ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r02/c2multi/traffic.json",
-                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r02/final/c3/traffic.json",
-                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r02/final/c2/traffic.json",
-                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r02/final/c4/traffic.json",
-                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r02/final/c2multi/traffic.json"}
+                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r03/final/c3/traffic.json",
+                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r03/final/c2/traffic.json",
+                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r03/final/c4/traffic.json",
+                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r03/final/c2multi/traffic.json"}
 
 
 def traffic_of(name, n, rec):
