@@ -621,6 +621,9 @@ def main():
             "config": {"workload": args.workload, "frames_per_gpu": wl.n,
                        "frame_len": wl.frame_len or "imix", "flows": wl.flows,
                        "tcbs": wl.flows + 1, "record_bytes": args.rec,
+                       "record_kind": {8: "RXG_REC8", 16: "RXG_REC16", 48: "RXG_REC48"}[args.rec] +
+                       " (record writes are not in the roofline's algorithmic bytes; the REC16 form is "
+                       "legs.c3_1500B_1Kflows_rec16)",
                        "bytes_per_gpu_step": wl.bytes_per_batch,
                        "parallelism": f"dp{world} (independent batches, replicated TCB mirror)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
