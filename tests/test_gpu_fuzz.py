@@ -8,6 +8,7 @@ make tcp_states.c-shaped writes (tests/test_gpu_replay.py Model).  Every packet'
 and the final table must equal the oracle run one packet at a time with the same writes
 at the same points."""
 import ctypes as C
+import os
 import random
 
 import pytest
@@ -74,7 +75,11 @@ def _post(engine, ops):
             assert engine.tcb_post_remove(i) == 0
 
 
-@pytest.mark.parametrize("seed,arp", [(101, False), (202, False), (303, True)])
+# RXG_FUZZ_SEEDS=<k> adds k more seeds (soak runs; the regular suite runs these three)
+_EXTRA = [(1000 + i, i % 3 == 0) for i in range(int(os.environ.get("RXG_FUZZ_SEEDS", "0")))]
+
+
+@pytest.mark.parametrize("seed,arp", [(101, False), (202, False), (303, True)] + _EXTRA)
 def test_random_bursts_equal_sequential_reference(replay_engine, seed, arp):
     engine = replay_engine
     """arp: the ARP mirror is on (half the sources known up front); the replay's add_mac

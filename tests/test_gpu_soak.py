@@ -1,0 +1,90 @@
+"""GPU soak (opt-in: RXG_SOAK=<seconds>): random parity batches over random launch shapes,
+compared bit-exact with the oracle until the time budget is spent.
+
+Each case draws a seed, a batch (the parity mixture of tests/pktgen.py: every size class,
+malformed frames, listeners, NULL slots, duplicate tuples, host-order dst), runs of <= 64 B
+frames of a few flows (the all-small path and its flow cache), a grid (rxg_config.max_blocks
+1..40: one to many slices per wave, so both the one- and the two-deep all-small pipelines
+run), a record kind, and single- or multi-burst launch.  Skipped unless RXG_SOAK is set: the
+round's regular GPU suite covers each path once; this is for hunting rare interleavings.
+"""
+import os
+import random
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+import pktgen
+import rxg
+
+pytestmark = pytest.mark.gpu
+BUDGET = float(os.environ.get("RXG_SOAK", "0"))
+
+
+@pytest.mark.skipif(BUDGET <= 0, reason="opt-in soak: set RXG_SOAK=<seconds>")
+def test_soak_random_launch_shapes():
+    t_end = time.time() + BUDGET
+    master = random.Random(int(os.environ.get("RXG_SOAK_SEED", "2026")))
+    engines = {}
+    cases = 0
+    try:
+        while time.time() < t_end:
+            seed = master.randrange(1 << 30)
+            rng = random.Random(seed)
+            n = rng.choice([1, 31, 64, 65, 200, 1000, 4096, 9000])
+            rows, frames = pktgen.parity_set(seed=seed, n=n, nflows=rng.choice([3, 50, 400]))
+            for _ in range(rng.randrange(0, 4)):  # runs of small frames of a few flows
+                a = rng.randrange(0, n)
+                for i in range(a, min(n, a + rng.randrange(64, 700))):
+                    frames[i] = pktgen.frame(src_ip=0x0A000001 + (i % 3), sport=1024 + (i % 3), dport=80,
+                                             payload=bytes(rng.randrange(0, 11)))
+            kind = rng.choice([rxg.REC8, rxg.REC16, rxg.REC48])
+            blocks = rng.choice([1, 2, 3, 5, 8, 13, 40])
+            if blocks not in engines:
+                engines[blocks] = rxg.Engine(device=0, max_batch=1 << 14, max_bytes=32 << 20, max_blocks=blocks)
+            eng = engines[blocks]
+            arena, off, lens = pktgen.pack_arena(frames)
+            tcb, live = pktgen.table_arrays(rows)
+            exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+            if kind == rxg.REC16:
+                exp = exp["c"]
+            elif kind == rxg.REC8:
+                exp = rxg.rec8_pack(exp["c"])
+            eng.tcb_load(tcb, live)
+            eng.counters_reset()
+            multi = n > 2 and rng.random() < 0.5
+            if not multi:
+                got = eng.rx_arena(arena, off, lens, kind)
+            else:
+                k = rng.randrange(2, min(n, 33))
+                cuts = [0] + sorted(rng.sample(range(1, n), k - 1)) + [n]
+                d_arena = eng.to_device(arena)
+                dev, bursts = [], []
+                try:
+                    for j in range(k):
+                        lo, hi = cuts[j], cuts[j + 1]
+                        do, dl = eng.to_device(off[lo:hi]), eng.to_device(lens[lo:hi])
+                        dout = eng.alloc((hi - lo) * kind)
+                        dev += [do, dl, dout]
+                        bursts.append((do.ptr, dl.ptr, hi - lo, dout.ptr))
+                    eng.rx_bursts_dev(d_arena.ptr, bursts, kind)
+                    eng.sync()
+                    got = np.concatenate([dev[3 * j + 2].download(rxg.rec_dtype(kind), cuts[j + 1] - cuts[j])
+                                          for j in range(k)])
+                finally:
+                    for d in dev + [d_arena]:
+                        d.free()
+            cnt = eng.counters()
+            assert got.tobytes() == exp.tobytes(), \
+                f"seed {seed} n {n} kind {kind} blocks {blocks} multi {multi}: records differ"
+            assert cnt.tolist() == ecnt.tolist(), f"seed {seed}: counters differ"
+            cases += 1
+            if cases % 50 == 0:
+                print(f"soak: {cases} cases", flush=True)  # progress (run with -s)
+    finally:
+        for e in engines.values():
+            e.close()
+    print(f"soak: {cases} cases bit-exact")
+    assert cases > 0
