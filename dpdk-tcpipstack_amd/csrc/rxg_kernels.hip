@@ -1192,6 +1192,30 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
         fc.src = src_host;
         fc.idx = idx;
         fc.meta = st | kFcValid;
+    } else if (is_tcp && !(STRIP & 2) && (STRIP & 33554432)) {
+        // experiment, timing only (variants 68 / 69): the first bucket's four slots compared
+        // straight-line; no second bucket; 69 (STRIP 67108864) adds the listener fallback
+        uint32_t v = kEmpty;
+#pragma unroll
+        for (int k = 0; k < kSlotsPerBucket; ++k) {
+            const bool m = P.s[k].x == ports && P.s[k].y == dst_raw && P.s[k].z == src_host;
+            v = m ? P.s[k].w : v;
+        }
+        if (v != kEmpty) {
+            idx = (int32_t)(v & kIdxMask);
+            st = v >> kStateShift;
+        } else if constexpr ((STRIP & 67108864) != 0) {
+            const int32_t L = a.t.listen[dport];
+            idx = L;
+            lhit = L >= 0;
+            nslot = a.t.min_null < (L >= 0 ? L : a.t.ntcb);
+            if (lhit) st = RXG_LISTENING;
+        }
+        fc.ports = ports;
+        fc.dst = dst_raw;
+        fc.src = src_host;
+        fc.idx = idx;
+        fc.meta = st | ((uint32_t)lhit << 8) | ((uint32_t)nslot << 9) | ((uint32_t)arp_learn << 10) | kFcValid;
     } else if (is_tcp && !(STRIP & 2) && (STRIP & 8388608)) {
         // experiment STRIP 8388608: the first bucket (already loaded and transposed) compared
         // straight-line by every lane; only lanes whose tuple may sit in a later bucket (first
@@ -2084,6 +2108,14 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
                 hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
             else
                 hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 68 && a.nbursts == 1) {  // timing only: straight-line first bucket, no fallback
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 33554432>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 69 && a.nbursts == 1) {  // timing only: + the listener fallback
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 33554432 | 67108864>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 67) {  // one-deep all-small pipeline whatever the launch length (round 2)
