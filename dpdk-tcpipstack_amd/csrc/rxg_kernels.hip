@@ -1576,7 +1576,14 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     // the one-flow C2 burst, which never probes, 19.2 -> 20.6 (more registers live across
     // the prefetch); the C2 configuration is the one the metric names.
     const Probe PO = ((STRIP & 2) || cached) ? probe_none() : probe_issue<STRIP>(a, true, F);
-    if (nxt) issue_small_slice<true>(a, n_off, n_len, lane, vb[1 - P]);
+    // The next slice's frames are issued whether or not the run continues (a run's last step
+    // reads the arena's first bytes instead): the compiler cannot count a load issued under a
+    // branch, and the probe's wait below then drained the prefetch too (64 B frames at 64 K
+    // flows 29.2 -> 28.3 us; STRIP 536870912, experiment 73, keeps the conditional form).
+    if constexpr ((STRIP & 536870912) == 0)
+        issue_small_slice<true>(a, nxt ? n_off : 0u, nxt ? n_len : 0u, lane, vb[1 - P]);
+    else if (nxt)
+        issue_small_slice<true>(a, n_off, n_len, lane, vb[1 - P]);
     uint32_t y_off, y_len;
     load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
     classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PO, wc, rec, fc, cached);
@@ -1617,7 +1624,10 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
     uint32_t z_off, z_len;
     load_desc<SEL, std::remove_reference_t<decltype(bc)>>(a, s + 3u * nwaves, lane, z_off, z_len, bc);
     const bool nxt2 = pend && s2 < nslices && slice_frames(a, uniform(s2), bc) == 64u && __ballot(y_len <= 64u) == ~0ull;
-    if (nxt2) issue_small_slice<true>(a, y_off, y_len, lane, vb[P]);
+    if constexpr ((STRIP & 536870912) == 0)  // unconditional, as in small_step
+        issue_small_slice<true>(a, nxt2 ? y_off : 0u, nxt2 ? y_len : 0u, lane, vb[P]);
+    else if (nxt2)
+        issue_small_slice<true>(a, y_off, y_len, lane, vb[P]);
     classify_finish<MODE, STRIP>(a, s * 64u + (uint32_t)lane, true, c_len, F, PO, wc, rec, fc, cached);
     bytes += c_len;
     if (!(STRIP & 4)) {
@@ -2108,6 +2118,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
                 hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
             else
                 hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 73 && a.nbursts == 1) {  // next-slice frames issued only when the run continues (round 2)
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 536870912>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 68 && a.nbursts == 1) {  // timing only: straight-line first bucket, no fallback
