@@ -95,17 +95,31 @@ RXG_HD uint32_t imix_len(int pos)
     return ((pat >> pos) & 1u) ? 576u : 64u;
 }
 
-// ARP mirror: open-addressing set of host-order IPv4 addresses, slot = {ip, used}.
-RXG_HD uint32_t arp_hash(uint32_t ip) { return tuple_hash(ip, 0x41525000u, 0u); }
+// ARP mirror: a set of host-order IPv4 addresses as buckets of four 4-byte keys (one 16-byte
+// load per probe), key 0 = free; the address 0 itself is a flag of the launch (DevTable).
+// Linear probing over buckets; a lookup ends at the first bucket holding a free key.
+constexpr int kArpKeysPerBucket = 4;
+RXG_HD uint32_t arp_hash(uint32_t ip)
+{
+    uint32_t h = ip ^ 0x41525000u;  // murmur3 finaliser: two multiplies
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+constexpr uint32_t kArpOn = 1u, kArpZero = 2u;  // DevTable::arp_flags
 
 struct DevTable {
     const uint4 *buckets;  // nbuckets * 4 slots
     const int32_t *listen; // 65536
-    const uint2 *arp;      // ARP mirror slots, or nullptr (mirror disabled)
+    const uint4 *arp;      // ARP mirror buckets (a valid 16-byte word even with the mirror off)
     uint32_t bucket_mask;  // nbuckets - 1
     int32_t ntcb;
     int32_t min_null;      // INT32_MAX if none
-    uint32_t arp_mask;     // ARP slots - 1
+    uint32_t arp_mask;     // ARP buckets - 1 (0 with the mirror off: every lane reads one word)
+    uint32_t arp_flags;    // kArpOn | kArpZero (0.0.0.0 is a member)
 };
 
 }  // namespace rxg

@@ -281,6 +281,12 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
         rxg_fini(c);
         return fail(-ENOMEM, "rxg_init: counters");
     }
+    // the ARP bucket every lane reads while the mirror is off (classify_finish issues the
+    // ARP probe unconditionally)
+    if (ensure(c->d_arp, 256) || hipMemset(c->d_arp.p, 0, c->d_arp.bytes) != hipSuccess) {
+        rxg_fini(c);
+        return fail(-ENOMEM, "rxg_init: ARP mirror");
+    }
     c->max_batch = cfg ? cfg->max_batch : 0;
     c->max_bytes = cfg ? cfg->max_bytes : 0;
     if (c->max_batch) {
@@ -540,7 +546,7 @@ static int apply_patches(rxg_ctx *c, M &mirror)
     int rc = wait_table_readers(c);
     if (rc) return rc;
     HIP_OK(launch_mirror_patch(pb.h, (uint32_t)p.size(), (uint4 *)c->buckets.p, (int32_t *)c->listen.p,
-                               (uint2 *)c->d_arp.p, c->stream));
+                               (uint32_t *)c->d_arp.p, c->stream));
     HIP_OK(hipEventRecord(pb.ev, c->stream));
     pb.set = true;
     HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
@@ -638,7 +644,7 @@ static int arp_sync(rxg_ctx *c)
     } else if ((rc = apply_patches(c, a))) {
         return rc;
     }
-    c->arp_mask = a.ns - 1;
+    c->arp_mask = a.nb - 1;
     c->arp_dirty = false;
     return 0;
 }
@@ -689,8 +695,9 @@ static DevTable table_view(const rxg_ctx *c)
     t.bucket_mask = c->bucket_mask;
     t.ntcb = c->dev_ntcb;
     t.min_null = c->dev_min_null;
-    t.arp = c->arp_enabled ? (const uint2 *)c->d_arp.p : nullptr;
-    t.arp_mask = c->arp_mask;
+    t.arp = (const uint4 *)c->d_arp.p;
+    t.arp_mask = c->arp_enabled ? c->arp_mask : 0u;
+    t.arp_flags = c->arp_enabled ? (kArpOn | (c->arp.has_zero ? kArpZero : 0u)) : 0u;
     return t;
 }
 

@@ -71,7 +71,7 @@ struct CounterDelta {
 };
 hipError_t launch_counters_add(unsigned long long *row, const CounterDelta &d, hipStream_t st);
 
-hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets, int32_t *listen, uint2 *arp,
+hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets, int32_t *listen, uint32_t *arp,
                                hipStream_t st);
 
 }  // namespace rxg

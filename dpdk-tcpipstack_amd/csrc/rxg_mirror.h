@@ -476,22 +476,25 @@ class TcbMirror {
     }
 };
 
-// ARP mirror: the set of host-order IPv4 addresses add_mac has added (arp.c:282-317), as an
-// open-addressing table of {ip, used} probed linearly.  Addresses are only added between
-// loads, so insertion patches one slot; past load 1/2 the table is rebuilt at twice the size.
+// ARP mirror: the set of host-order IPv4 addresses add_mac has added (arp.c:282-317), as
+// buckets of four keys (rxg_common.h), key 0 = free, probed linearly by bucket; 0.0.0.0 is a
+// flag instead (has_zero).  Addresses are only added between loads, so insertion patches
+// one key; past load 1/2 the table is rebuilt at twice the size.
 class ArpMirror {
   public:
     std::vector<uint32_t> ips;  // add_mac order
     std::unordered_set<uint32_t> set;
-    std::vector<uint32_t> slots;  // ns x {ip, used}
-    uint32_t ns = 0;
+    std::vector<uint32_t> slots;  // nb x kArpKeysPerBucket keys
+    uint32_t nb = 0;
+    bool has_zero = false;
     bool need_rebuild = true;
-    std::vector<MirrorPatch> patches;  // one per slot (a slot is written once between loads)
+    std::vector<MirrorPatch> patches;  // one per key (a key is written once between loads)
 
     void clear()
     {
         ips.clear();
         set.clear();
+        has_zero = false;
         need_rebuild = true;
         patches.clear();
     }
@@ -503,34 +506,64 @@ class ArpMirror {
     {
         if (!set.insert(ip).second) return false;
         ips.push_back(ip);
+        if (ip == 0u) {
+            has_zero = true;  // travels in the launch's arguments, no table word
+            return true;
+        }
         if (need_rebuild) return true;
-        if ((uint64_t)ips.size() * 2u > ns) {
+        if ((uint64_t)ips.size() * 2u > (uint64_t)nb * kArpKeysPerBucket) {
             need_rebuild = true;
             return true;
         }
-        const uint32_t h = insert(ip);
-        patches.push_back(MirrorPatch{kPatchArp, h, {ip, 1u, 0u, 0u}});
+        const uint32_t w = insert(ip);
+        patches.push_back(MirrorPatch{kPatchArp, w, {ip, 0u, 0u, 0u}});
         return true;
     }
 
     void rebuild()
     {
-        ns = 16;
-        while ((uint64_t)ns < (uint64_t)ips.size() * 2u) ns <<= 1;
-        slots.assign((size_t)ns * 2u, 0u);
-        for (uint32_t ip : ips) insert(ip);
+        nb = 4;
+        while ((uint64_t)nb * kArpKeysPerBucket < (uint64_t)ips.size() * 2u) nb <<= 1;
+        slots.assign((size_t)nb * kArpKeysPerBucket, 0u);
+        for (uint32_t ip : ips)
+            if (ip) insert(ip);
         need_rebuild = false;
         patches.clear();
     }
 
+    // the kernel's lookup (classify_finish) over a copy of the keys
+    static bool lookup(const uint32_t *keys, uint32_t nb, bool has_zero, uint32_t ip)
+    {
+        if (ip == 0u) return has_zero;
+        uint32_t b = arp_hash(ip) & (nb - 1);
+        for (uint32_t p = 0; p < nb; ++p) {
+            bool free = false;
+            for (int k = 0; k < kArpKeysPerBucket; ++k) {
+                const uint32_t x = keys[(size_t)b * kArpKeysPerBucket + k];
+                if (x == ip) return true;
+                free |= x == 0u;
+            }
+            if (free) return false;
+            b = (b + 1) & (nb - 1);
+        }
+        return false;
+    }
+
   private:
+    // the key's word index
     uint32_t insert(uint32_t ip)
     {
-        uint32_t h = arp_hash(ip) & (ns - 1);
-        while (slots[(size_t)h * 2 + 1]) h = (h + 1) & (ns - 1);
-        slots[(size_t)h * 2] = ip;
-        slots[(size_t)h * 2 + 1] = 1;
-        return h;
+        uint32_t b = arp_hash(ip) & (nb - 1);
+        for (;;) {
+            for (int k = 0; k < kArpKeysPerBucket; ++k) {
+                const size_t w = (size_t)b * kArpKeysPerBucket + k;
+                if (slots[w] == 0u) {
+                    slots[w] = ip;
+                    return (uint32_t)w;
+                }
+            }
+            b = (b + 1) & (nb - 1);
+        }
     }
 };
 

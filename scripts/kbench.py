@@ -66,7 +66,7 @@ def main():
     # A variant may name another build of librxg (4th field, a path): A/B of two builds in
     # one process.  The binding's module-level library handle is switched per engine.
     main_lib = rxg.load_library()
-    libs, engines = {}, {}
+    libs, engines, arp_on = {}, {}, {}
     for v in args.variants.split(","):
         parts = v.split(":")
         os.environ["RXG_VARIANT"] = parts[0]
@@ -80,6 +80,9 @@ def main():
             lib = rxg.load_library(parts[3])
         rxg._lib = lib
         libs[v] = lib
+        # 6th field "arp": the ARP mirror on, loaded with every flow's source (ip.c:30-32 finds
+        # them all: the kernel's ARP probe runs, RXG_F_ARP_LEARN stays clear)
+        arp_on[v] = len(parts) > 5 and parts[5] == "arp"
         engines[v] = rxg.Engine(0)
         rxg._lib = main_lib
     res = {(v, w): [] for v in engines for w in wls}
@@ -88,6 +91,8 @@ def main():
             for v, eng in engines.items():
                 rxg._lib = libs[v]
                 eng.tcb_load(tcb, live)
+                if arp_on[v]:
+                    eng.arp_load(tcb["ipv4_src"][1:])
                 eng.tcb_sync()
                 evs = [(eng.event(), eng.event()) for _ in range(args.iters)]
                 def launch(b):
@@ -119,6 +124,8 @@ def main():
             for v, eng in engines.items():
                 rxg._lib = libs[v]
                 eng.tcb_load(tcb, live)
+                if arp_on[v]:
+                    eng.arp_load(tcb["ipv4_src"][1:])
                 eng.tcb_sync()
                 eng.counters_reset()
                 if w == "c2m":

@@ -65,10 +65,8 @@ static void sync_dev(TcbMirror &m, ArpMirror &a, Dev &d, uint64_t &nrebuild, uin
             d.slots[q.index] = Slot{q.v[0], q.v[1], q.v[2], q.v[3]};
         else if (q.target == kPatchListen)
             d.listen[q.index] = (int32_t)q.v[0];
-        else {
-            d.arp[(size_t)q.index * 2] = q.v[0];
-            d.arp[(size_t)q.index * 2 + 1] = q.v[1];
-        }
+        else
+            d.arp[q.index] = q.v[0];
     }
 }
 
@@ -167,6 +165,7 @@ int main(int argc, char **argv)
     }
     std::vector<uint32_t> arp_pool(4096);
     for (auto &x : arp_pool) x = (uint32_t)rng();
+    arp_pool[0] = 0u;  // 0.0.0.0: a flag of the launch, not a key
     for (int b = 0; b < 64; ++b) a.add(arp_pool[(size_t)R(arp_pool.size())]);
     sync_dev(m, a, d, nrebuild, npatch);
 
@@ -224,17 +223,8 @@ int main(int argc, char **argv)
         }
         // ARP membership
         for (int q = 0; q < 8; ++q) {
-            const uint32_t ip = arp_pool[(size_t)R(arp_pool.size())];
-            uint32_t h = arp_hash(ip) & (a.ns - 1);
-            bool found = false;
-            for (uint32_t p = 0; p < a.ns; ++p) {
-                if (!d.arp[(size_t)h * 2 + 1]) break;
-                if (d.arp[(size_t)h * 2] == ip) {
-                    found = true;
-                    break;
-                }
-                h = (h + 1) & (a.ns - 1);
-            }
+            const uint32_t ip = q ? arp_pool[(size_t)R(arp_pool.size())] : 0u;
+            const bool found = ArpMirror::lookup(d.arp.data(), a.nb, a.has_zero, ip);
             CHECK(found == (a.set.count(ip) != 0), "ARP membership of %08x", ip);
         }
         if (fails) break;

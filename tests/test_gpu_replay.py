@@ -244,3 +244,62 @@ def test_replay_refused_after_a_failed_burst(engine):
         engine.rx_burst(big, rxg.REC16)
     assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, n, 16) == -22
     assert b"failed" in lib.rxg_last_error()
+
+
+def _arp_hash(ip):
+    """rxg_common.h arp_hash (murmur3 finaliser), to build bucket clusters on purpose."""
+    M = 0xFFFFFFFF
+    h = (ip ^ 0x41525000) & M
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M
+    return h ^ (h >> 16)
+
+
+def test_arp_bucket_clusters_and_zero(engine):
+    """The ARP mirror's bucketed probe: addresses whose first bucket is full (clusters over
+    several buckets, found and not found), 0.0.0.0 (a launch flag, not a key), additions by
+    patch (rxg_arp_learned) and by rebuild, over small-frame and streaming slices."""
+    rng = random.Random(31)
+    def nb_for(n):
+        nb = 4
+        while nb * 4 < 2 * n:
+            nb <<= 1
+        return nb
+    # 40 known: 14 with first bucket 5 (fill buckets 5..8), the rest anywhere
+    mask = nb_for(40) - 1
+    pool = [pktgen.ip4(10, 77, rng.randrange(256), rng.randrange(1, 256)) for _ in range(20000)]
+    pool = list(dict.fromkeys(pool))
+    clus = [ip for ip in pool if _arp_hash(ip) & mask == 5]
+    assert len(clus) >= 30
+    known = clus[:14] + [ip for ip in pool if _arp_hash(ip) & mask != 5][:26]
+    unknown = clus[14:24] + [ip for ip in pool if ip not in known][100:120] + [0]
+    srcs = known + unknown
+    frames = [pktgen.frame(src_ip=rng.choice(srcs), sport=rng.randrange(1024, 65536), flags=0x10,
+                           payload=bytes(rng.choice([0, 0, 0, 10, 600, 1400]))) for _ in range(3000)]
+    tcb, live = pktgen.table_arrays([(80, 0, pktgen.raw_of_host(pktgen.ip4(192, 168, 78, 2)), 0, 1)])
+    engine.tcb_load(tcb, live)
+    engine.arp_load(known)
+
+    def check(members):
+        for kind in (rxg.REC16, rxg.REC8):
+            recs = engine.rx_burst(frames, kind)
+            if kind == rxg.REC8:
+                fl = (recs["w1"] >> 8) & 0x3F
+            else:
+                fl = recs["flags"]
+            got = (fl & rxg.F_ARP_LEARN) != 0
+            exp = np.array([int.from_bytes(f[26:30], "big") not in members for f in frames])
+            assert (got == exp).all(), (kind, np.flatnonzero(got != exp)[:8])
+
+    check(set(known))
+    for ip in clus[14:24]:              # patches into the cluster (no rebuild: load <= 1/2)
+        engine.arp_learned(ip)
+    check(set(known) | set(clus[14:24]))
+    engine.arp_learned(0)
+    check(set(known) | set(clus[14:24]) | {0})
+    for ip in pool[:200]:               # past load 1/2: rebuilt at a larger size
+        engine.arp_learned(ip)
+    check(set(known) | set(clus[14:24]) | {0} | set(pool[:200]))
+    engine.arp_disable()
