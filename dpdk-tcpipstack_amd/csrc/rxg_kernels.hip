@@ -1160,6 +1160,27 @@ __device__ __forceinline__ Probe probe_from_lds(const RxArgs &a, const Fields &F
     return P;
 }
 
+// One 64-byte bucket through the scalar data cache into SGPRs (uniform address).  Its wait
+// is on lgkmcnt, not vmcnt: the vector loads in flight (the next slice's frames) are not
+// drained, as a vector load consumed right after issue would drain them (vmcnt retires in
+// order).  Read only; the table is not written during a launch.
+__device__ __forceinline__ void sload_bucket(const uint4 *b, uint32_t (&x)[16])
+{
+    typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+    u32x16 r;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(b));
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = r[k];
+}
+
+__device__ __forceinline__ uint4 sload_arp_bucket(const uint4 *b)
+{
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(b));
+    return make_uint4(r.x, r.y, r.z, r.w);
+}
+
 template <int MODE, int STRIP>
 __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, bool valid, uint32_t len,
                                                 const Fields &F, const Probe &P, WaveCounters &wc,
@@ -1176,23 +1197,28 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
     const bool trunc = valid && len < 54u;
     // ip.c:30-32: would get_mac(ntohl(src)) fail?  (ARP mirror enabled only)  The first
     // bucket came with the probe (P.arp); lanes whose address may sit in a later bucket
-    // (first bucket full, no match) walk on, under a wave-uniform test.
+    // (first bucket full, no match) are walked one at a time by scalar loads, as the TCB
+    // probe's overflow below.
     bool arp_learn = false;
     if (is_tcp && (a.t.arp_flags & kArpOn) && !cached) {
         const uint32_t ip = bswap32(src_raw);
         const uint4 k = P.arp;
         bool hit = k.x == ip || k.y == ip || k.z == ip || k.w == ip;
         const bool more = ip != 0u && !hit && k.x && k.y && k.z && k.w;
-        if (__ballot(more) != 0ull) {
-            if (more) {
-                uint32_t b = arp_hash(ip) & a.t.arp_mask;
-                for (uint32_t probe = 1; probe <= a.t.arp_mask; ++probe) {
-                    b = (b + 1u) & a.t.arp_mask;
-                    const uint4 e = a.t.arp[b];
-                    hit = e.x == ip || e.y == ip || e.z == ip || e.w == ip;
-                    if (hit || !e.x || !e.y || !e.z || !e.w) break;
-                }
+        unsigned long long need = __ballot(more);
+        while (need != 0ull) {  // wave-uniform
+            const int l = (int)__builtin_ctzll(need);
+            need &= need - 1ull;
+            const uint32_t ipl = __builtin_amdgcn_readlane(ip, l);
+            uint32_t b = arp_hash(ipl) & a.t.arp_mask;
+            bool h = false;
+            for (uint32_t probe = 1; probe <= a.t.arp_mask; ++probe) {
+                b = (b + 1u) & a.t.arp_mask;
+                const uint4 e = sload_arp_bucket(a.t.arp + b);
+                h = e.x == ipl || e.y == ipl || e.z == ipl || e.w == ipl;
+                if (h || !e.x || !e.y || !e.z || !e.w) break;
             }
+            if ((int)(threadIdx.x & 63u) == l) hit = h;
         }
         arp_learn = ip == 0u ? !(a.t.arp_flags & kArpZero) : !hit;
     }
@@ -1290,7 +1316,60 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, uint32_t f, boo
         fc.src = src_host;
         fc.idx = idx;
         fc.meta = st | ((uint32_t)lhit << 8) | ((uint32_t)nslot << 9) | ((uint32_t)arp_learn << 10) | kFcValid;
-    } else if (is_tcp && !(STRIP & 2)) {
+    } else if (is_tcp && !(STRIP & 2) && !(STRIP & 1073741824)) {
+        // The first bucket (loaded with the probe) compared straight-line by every lane; lanes
+        // whose tuple may sit in a later bucket (first bucket full, no match: ~0.4 % of the
+        // lanes at 64 K flows, a quarter of the slices) are walked one at a time by the whole
+        // wave through scalar loads (sload_bucket).  The walk waits on lgkmcnt, so the next
+        // slice's frames stay in flight; the round-2 per-lane loop (STRIP 1073741824,
+        // variant 74) consumed a vector load right after issue, which drained them: C4
+        // 74.6 -> 73.6 us, 64 B frames at 64 K flows 28.7 -> 27.5.
+        uint32_t v = kEmpty;
+        bool empty = false;
+#pragma unroll
+        for (int k = 0; k < kSlotsPerBucket; ++k) {
+            const bool m = P.s[k].x == ports && P.s[k].y == dst_raw && P.s[k].z == src_host;
+            v = m ? P.s[k].w : v;  // a free slot holds kEmpty: a match there is no hit
+            empty |= P.s[k].w == kEmpty;
+        }
+        unsigned long long need = __ballot(v == kEmpty && !empty);
+        while (need != 0ull) {  // wave-uniform
+            const int l = (int)__builtin_ctzll(need);
+            need &= need - 1ull;
+            const uint32_t kp = __builtin_amdgcn_readlane(ports, l), kd = __builtin_amdgcn_readlane(dst_raw, l);
+            const uint32_t ks = __builtin_amdgcn_readlane(src_host, l);
+            uint32_t hb = __builtin_amdgcn_readlane(P.hb, l), w = kEmpty;
+            for (uint32_t probe = 1; probe <= a.t.bucket_mask; ++probe) {
+                hb = (hb + 1u) & a.t.bucket_mask;
+                uint32_t x[16];
+                sload_bucket(a.t.buckets + (size_t)hb * kSlotsPerBucket, x);
+                bool e2 = false;
+#pragma unroll
+                for (int k = 0; k < kSlotsPerBucket; ++k) {
+                    if (x[4 * k] == kp && x[4 * k + 1] == kd && x[4 * k + 2] == ks && x[4 * k + 3] != kEmpty)
+                        w = x[4 * k + 3];
+                    e2 |= x[4 * k + 3] == kEmpty;
+                }
+                if (w != kEmpty || e2) break;
+            }
+            if ((int)(threadIdx.x & 63u) == l) v = w;
+        }
+        if (v != kEmpty) {
+            idx = (int32_t)(v & kIdxMask);
+            st = v >> kStateShift;
+        } else {  // pass 2: first LISTENING slot on dport (its state is LISTENING)
+            const int32_t L = a.t.listen[dport];
+            idx = L;
+            lhit = L >= 0;
+            nslot = a.t.min_null < (L >= 0 ? L : a.t.ntcb);
+            if (lhit) st = RXG_LISTENING;
+        }
+        fc.ports = ports;
+        fc.dst = dst_raw;
+        fc.src = src_host;
+        fc.idx = idx;
+        fc.meta = st | ((uint32_t)lhit << 8) | ((uint32_t)nslot << 9) | ((uint32_t)arp_learn << 10) | kFcValid;
+    } else if (is_tcp && !(STRIP & 2)) {  // experiment STRIP 1073741824: the round-2 per-lane loop
         uint32_t hb = P.hb;
         uint4 sl[kSlotsPerBucket];
 #pragma unroll
@@ -2146,6 +2225,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
                 hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576, false, 11, true>), dim3(blocks), dim3(256), 0, st, a);
             else
                 hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a);
+            return hipGetLastError();
+        }
+        if (L.variant == 74 && a.nbursts == 1) {  // the round-2 per-lane bucket loop (vector loads)
+            hipLaunchKernelGGL((rx_kernel<8, 0xFF, true, 1073741824>), dim3(blocks), dim3(256), 0, st, a);
             return hipGetLastError();
         }
         if (L.variant == 73 && a.nbursts == 1) {  // next-slice frames issued only when the run continues (round 2)

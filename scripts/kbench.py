@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--frames-c2", type=int, default=0, help="override frames for c2* workloads")
     ap.add_argument("--rec", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=77, help="copy c is synthesised with seed + c * seed_step")
+    ap.add_argument("--seed-step", type=int, default=1, help="17 with bench.py's seed reproduces its batches")
     ap.add_argument("--tx", action="store_true", help="time rxg_tx_cksum_dev (rx_kernel<0>) instead")
     ap.add_argument("--check", action="store_true",
                     help="also compare every variant's records (and counters) with the first variant's")
@@ -54,7 +56,7 @@ def main():
             tcb, live = rxg.synthetic_tcb_table(1)
             wls[w] = ([pool], nfr * MULTI * 64, tcb, live, nfr)
             continue
-        bs = [base.synth(n=nfr, nflows=flows, len_a=L or 1500, mix=mix, seed=77 + c)
+        bs = [base.synth(n=nfr, nflows=flows, len_a=L or 1500, mix=mix, seed=args.seed + c * args.seed_step)
               for c in range(copies)]
         lens = bs[0]["len"].download(np.uint16, nfr)
         tcb, live = rxg.synthetic_tcb_table(flows)
@@ -113,7 +115,7 @@ def main():
                     eng.record(evs[i][1])
                 eng.sync()
                 ms = [eng.elapsed_ms(a, b) for a, b in evs]
-                res[(v, w)].append(float(np.median(ms)))
+                res[(v, w)].append(ms)
                 for a, b in evs:
                     libs[v].rxg_event_destroy(eng.ctx, a)
                     libs[v].rxg_event_destroy(eng.ctx, b)
@@ -145,9 +147,12 @@ def main():
                                   "counters_equal": got[1] == ref[1]}), flush=True)
     for (v, w), ms in res.items():
         nbytes = wls[w][1]
-        med = float(np.median(ms))
+        med = float(np.median([np.median(r) for r in ms]))  # median over rounds of each round's median
+        allm = [x for r in ms for x in r]
         print(json.dumps({"variant": v, "workload": w, "kernel_us_median": round(med * 1e3, 2),
-                          "kernel_us_min": round(min(ms) * 1e3, 2),
+                          "kernel_us_min": round(min(np.median(r) for r in ms) * 1e3, 2),
+                          "kernel_us_mean_all": round(float(np.mean(allm)) * 1e3, 2),
+                          "kernel_us_max_all": round(max(allm) * 1e3, 2),
                           "GBps": round(nbytes / (med * 1e-3) / 1e9, 1),
                           "frac_8TBs": round(nbytes / (med * 1e-3) / 8e12, 4)}), flush=True)
 
