@@ -541,11 +541,23 @@ __device__ __forceinline__ void full_sum(const uint32_t (&q)[4], uint32_t w, uin
     t[3] = dsum(q[3], w, t[3]);
 }
 
+// Tx (MODE 0) with deferred line writes (SV 7): a frame over 64 bytes is not rewritten when
+// its round is summed; its leader appends {off64, the two checksums as stored} to the wave's
+// LDS queue, and tx_flush rewrites the queued frames' first 64-byte lines together, at the
+// wave's end (or when the queue is full).  The writes then leave the read stream, as the
+// rx kernel's records do (record ring).
+constexpr int kTxqCap = 512;  // entries per wave (8 slices of frames over 64 bytes)
+struct TxQ {
+    uint2 *buf;   // this wave's kTxqCap entries {off64, bswap16(ip_ck) | bswap16(tcp_ck) << 16}
+    uint32_t n;   // wave-uniform
+};
+
 // A frame of <= 64 bytes owned by one lane: q = its four chunks as loaded (bytes at or past
 // data_len may hold anything: every use below masks them).  Same results as
 // frame_fields<1, 4, ...>, fewer instructions.
-template <int MODE, bool LINE64 = false>
-__device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32_t (&q)[4][4])
+template <int MODE, bool LINE64 = false, bool DQ = false>
+__device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32_t (&q)[4][4], uint32_t off64 = 0u,
+                                               TxQ *tq = nullptr)
 {
     constexpr bool TX = MODE == 0;
     uint32_t h1 = q[0][1], h2 = q[0][2], h3 = q[0][3], h4 = q[1][0], h5 = q[1][1], h6 = q[1][2];
@@ -596,7 +608,19 @@ __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32
         // beyond data_len are never written.  Two 2-byte stores: rewriting a 64-byte frame's
         // whole line instead (LINE64, experiment variant 24) measured slower, C4 tx 101.4
         // against 94.5 us, 64 B frames 40.9 against 33.6 (the write bytes count).
-        if (LINE64 && len == 64u) {
+        bool inl = true;
+        if constexpr (DQ) {  // 64-byte frames queued: tx_flush rewrites their line (TxQ)
+            const bool dq = len == 64u;
+            const unsigned long long lm = __ballot(dq);
+            if (dq) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+                tq->buf[tq->n + r] = make_uint2(off64, bswap16(ip_ck) | (bswap16(tcp_ck) << 16));
+            }
+            tq->n += (uint32_t)__popcll(lm);
+            inl = !dq;
+        }
+        if (!inl) {
+        } else if (LINE64 && len == 64u) {
             uint4 *l = reinterpret_cast<uint4 *>(fp);
             l[0] = make_uint4(q[0][0], q[0][1], q[0][2], q[0][3]);
             l[1] = make_uint4(q[1][0], q[1][1], (q[1][2] & 0xFFFF0000u) | bswap16(ip_ck), q[1][3]);
@@ -635,23 +659,57 @@ __device__ __forceinline__ void round_load(const RxArgs &a, uint32_t off, uint32
     }
 }
 
+// Rewrite the first 64-byte line of every queued frame: the line as it is in memory with the
+// two checksum fields (bytes 24-25, 50-51) set.  16 frames per instruction (lane l: chunk l&3
+// of entry 16j + l/4), four instructions in flight.  Whole-wave call.
+__device__ __forceinline__ void tx_flush(const RxArgs &a, TxQ &q, int lane)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t n = q.n;
+    uint8_t *frames = const_cast<uint8_t *>(a.frames);
+    const int ch = lane & 3;
+    for (uint32_t g = 0; g < n; g += 64u) {
+        uint4 v[4];
+        uint32_t ck[4];
+        uint8_t *p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = min(g + 16u * j + (uint32_t)(lane >> 2), n - 1u);
+            const uint2 E = q.buf[e];
+            p[j] = frames + (size_t)E.x * 64u + ch * 16;
+            ck[j] = E.y;
+            v[j] = *reinterpret_cast<const uint4 *>(p[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (ch == 1) v[j].z = (v[j].z & 0xFFFF0000u) | (ck[j] & 0xFFFFu);   // bytes 24-25
+            if (ch == 3) v[j].x = (v[j].x & 0x0000FFFFu) | (ck[j] & 0xFFFF0000u);  // bytes 50-51
+            if (g + 16u * j + (uint32_t)(lane >> 2) < n) *reinterpret_cast<uint4 *>(p[j]) = v[j];
+        }
+    }
+    q.n = 0;
+    __builtin_amdgcn_wave_barrier();  // queue reads before the next slice's appends
+}
+
 template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV = 0>
 __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
-                                                      int lane, uint32_t (&d)[NLOAD][4]);
+                                                      int lane, uint32_t (&d)[NLOAD][4], TxQ *q = nullptr);
 
 template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV = 0>
 __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off, uint32_t len, bool active,
-                                                   int lane)
+                                                   int lane, TxQ *q = nullptr)
 {
     uint32_t d[NLOAD][4];
     round_load<C, LPF, NLOAD, NT>(a, off, len, lane, d);
-    return frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, off, len, active, lane, d);
+    return frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, off, len, active, lane, d, q);
 }
 
 // Sums, header fields and (tx) checksum stores of one round whose chunks are in d.
 template <int C, int LPF, int NLOAD, int MODE, bool NT, int SV>
 __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
-                                                      int lane, uint32_t (&d)[NLOAD][4])
+                                                      int lane, uint32_t (&d)[NLOAD][4], TxQ *q)
 {
     static_assert(LPF >= 2 && LPF <= 64, "streaming classes only");
     constexpr bool TX = MODE == 0;
@@ -743,7 +801,15 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
-    if constexpr (TX) {
+    if constexpr (TX && SV == 7) {
+        // deferred: the leader queues the frame; tx_flush writes its line (see TxQ)
+        const unsigned long long lm = __ballot(leader);
+        if (leader) {
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+            q->buf[q->n + r] = make_uint2(off, bswap16(ip_ck) | (bswap16(tcp_ck) << 16));
+        }
+        q->n += (uint32_t)__popcll(lm);
+    } else if constexpr (TX) {
         // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118).  Frames of
         // these classes are longer than 64 bytes: the group writes the frame's whole first
         // 64-byte line (chunks 0-3, as loaded, with the two checksum fields set) rather
@@ -784,7 +850,7 @@ __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int l
 
 template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int SV = 0, bool PIPE = false>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
-                                          int lane_in, uint32_t *sf)
+                                          int lane_in, uint32_t *sf, TxQ *q = nullptr)
 {
     constexpr int FPW = 64 / LPF;
     const unsigned long long m = __ballot(cls == C);
@@ -834,7 +900,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             const bool bact = rmeta(r + FPW, bo, boff, blen);
             round_load<C, LPF, NLOAD, NT>(a, boff, blen, lane, dB);
             {
-                const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, aoff, alen, aact, lane, dA);
+                const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, aoff, alen, aact, lane, dA, q);
                 if constexpr (MODE != 0) {
                     if (aact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, ao, F);
                 }
@@ -842,7 +908,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             aact = rmeta(r + 2u * FPW, ao, aoff, alen);
             round_load<C, LPF, NLOAD, NT>(a, aoff, alen, lane, dA);
             if (r + FPW < cnt) {
-                const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, boff, blen, bact, lane, dB);
+                const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT, SV>(a, boff, blen, bact, lane, dB, q);
                 if constexpr (MODE != 0) {
                     if (bact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, bo, F);
                 }
@@ -883,13 +949,14 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             uint32_t d[4][4];
             // (MODE 0, tx: no parked fields; the transpose uses the 4 KiB ring area itself)
             transpose_small_slice(v, rl, sf + (MODE == 0 ? 0 : MODE == 48 ? NF48 * 64 : NF16 * 64), d);
-            F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
+            F = fields_small<MODE, false, SV == 8>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d,
+                                                   koff, q);
         } else if constexpr (LPF == 1) {
             uint32_t d[4][4];
             load_chunks<1, 4, NT>(a, koff, act ? klen : 0u, act, rl, d);
             F = fields_small<MODE, SV == 4>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
         } else if constexpr (LPF >= 2 && !JUMBO)
-            F = frame_round_fast<C, LPF, NLOAD, MODE, NT, SV>(a, act ? koff : 0u, act ? klen : 0u, act, rl);
+            F = frame_round_fast<C, LPF, NLOAD, MODE, NT, SV>(a, act ? koff : 0u, act ? klen : 0u, act, rl, q);
         else
             F = frame_round<LPF, NLOAD, JUMBO, MODE, NT>(a, koff, act ? klen : 0u, act, rl);
         if constexpr (MODE != 0) {
@@ -1751,7 +1818,9 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
 }
 
 template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
-          bool DEFER = false, bool DTOP = true, int WPE = 0, bool DEEP = false>
+          bool DEFER = false, bool DTOP = true, int WPE = 0, bool DEEP = false, int TXD = 0>
+// TXD (tx, MODE 0): frames over 64 bytes (TXD 1), and 64-byte ones too (TXD 2), get their
+// first line rewritten by tx_flush, not in their round (TxQ).
 // WPE 0: no bound, except 3 waves per SIMD (at most 168 VGPRs) for rx kernels with the
 // software-pipelined rounds (experiment STRIP 32768), which would otherwise take 170 and drop to 2.
 // DEEP: runs of all-small slices prefetched two slices deep (small_step2); launch_rx picks it
@@ -1773,6 +1842,8 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
     __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kSlot];
     __shared__ uint32_t s_recf[4][RS];
     __shared__ __attribute__((aligned(16))) uint4 s_pb[DEFER ? 4 : 1][kSlotsPerBucket][DEFER ? 64 : 1];
+    static_assert(!TXD || MODE == 0, "deferred line writes: tx only");
+    __shared__ uint2 s_txq[TXD ? 4 : 1][TXD ? kTxqCap : 1];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
@@ -1787,6 +1858,7 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
     ring.base = s_recf[wid];
     Rec rec;
     FlowCache fcache;
+    TxQ txq{s_txq[TXD ? wid : 0], 0u};
 
     // Descriptors: (c_off, c_len) for slice s, (n_off, n_len) for slice s + nwaves, whose
     // loads are always in flight while slice s is processed.
@@ -1872,6 +1944,9 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         // were still in flight there, where the register copies c <- n <- y made the wave
         // wait for them (an s_waitcnt vmcnt(0) per slice in the ISA).
         uint32_t y_off = 0u, y_len = 0u;
+        if constexpr (TXD) {
+            if (txq.n > (uint32_t)(kTxqCap - 64)) tx_flush(a, txq, lane);
+        }
         if constexpr (DTOP) load_desc<SEL, std::remove_reference_t<decltype(bc)>, (STRIP & 524288) != 0>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
         if constexpr (DEFER) {
             if (d_issue) {
@@ -1887,7 +1962,9 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         constexpr bool NTS = NT && (STRIP & 131072) != 0;
         // 257-576 B classes: non-temporal; STRIP 262144 (experiment): plain
         constexpr bool NTM = NT && (STRIP & 262144) == 0;
-        constexpr int SVS = (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : 0;
+        constexpr int SVS = (STRIP & 64) ? 1 : (STRIP & 128) ? 2 : (STRIP & 256) ? 3 : (STRIP & 512) ? 4 : (STRIP & 1024) ? 5 : TXD ? 7 : 0;
+        constexpr int SV12 = TXD ? 7 : 0;
+        TxQ *const tq = TXD ? &txq : nullptr;
         // The streaming classes' rounds software-pipelined; STRIP 8192
         // (experiment) = the round-2 form.  Multi-burst kernels keep that form: with the burst
         // table held in lanes the pipelined rounds need 176 VGPRs (2 waves per SIMD); so do
@@ -1903,16 +1980,16 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         if constexpr (C0DMA) {
             if (m0 != 0ull) class0_issue_lds(a, m0, off, len, lane, t0);
         } else if constexpr ((CMASK >> 0) & 1) {
-            run_class<0, 1, 4, false, MODE, NTS, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : 0>(a, cls, off, len, lane, sf);
+            run_class<0, 1, 4, false, MODE, NTS, (STRIP & 512) ? 4 : (STRIP & 2048) ? 6 : TXD >= 2 ? 8 : 0>(a, cls, off, len, lane, sf, tq);
         }
-        if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, NTS, 0, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, NTS, 0, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NTM, SVS, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NTM, SVS, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
-        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf);
+        if constexpr ((CMASK >> 1) & 1) run_class<1, 2, 4, false, MODE, NTS, SV12, PIPE>(a, cls, off, len, lane, sf, tq);
+        if constexpr ((CMASK >> 2) & 1) run_class<2, 4, 4, false, MODE, NTS, SV12, PIPE>(a, cls, off, len, lane, sf, tq);
+        if constexpr ((CMASK >> 3) & 1) run_class<3, 8, 4, false, MODE, NTM, SVS, PIPE>(a, cls, off, len, lane, sf, tq);
+        if constexpr ((CMASK >> 4) & 1) run_class<10, 8, 5, false, MODE, NTM, SVS, PIPE>(a, cls, off, len, lane, sf, tq);
+        if constexpr ((CMASK >> 4) & 1) run_class<8, 8, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf, tq);
+        if constexpr ((CMASK >> 4) & 1) run_class<4, 16, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf, tq);
+        if constexpr ((CMASK >> 5) & 1) run_class<5, 16, 6, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf, tq);
+        if constexpr ((CMASK >> 6) & 1) run_class<6, 32, 4, false, MODE, NT, SVS, PIPE>(a, cls, off, len, lane, sf, tq);
         if constexpr ((CMASK >> 7) & 1) run_class<7, 64, 2, true, MODE, NT>(a, cls, off, len, lane, sf);
         if constexpr (C0DMA) {
             if (m0 != 0ull) class0_finish_lds<MODE>(a, m0, off, len, lane, sf, t0);
@@ -1963,6 +2040,7 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
     }
     finish_pending();
     if constexpr (MODE != 0) ring.flush(a, lane, bc);
+    if constexpr (TXD) tx_flush(a, txq, lane);
 
     if (a.counters == nullptr) return;
     // wave -> workgroup -> one atomic per counter
@@ -2344,6 +2422,10 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 256>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 52)  // the last generation's slices cut into pieces
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 1048576>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 75)  // frames over 64 B: lines rewritten at the wave's end (TxQ)
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 0, false, 11, false, false, true, 0, false, 1>), dim3(blocks), dim3(256), 0, st, a);
+        else if (L.variant == 76)  // the same for 64-byte frames too
+            hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 0, false, 11, false, false, true, 0, false, 2>), dim3(blocks), dim3(256), 0, st, a);
         else if (L.variant == 32)  // descriptors loaded at the slice's end (round-2 start)
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true, 0, false, 11, false, false, false>), dim3(blocks), dim3(256), 0, st, a);
         else

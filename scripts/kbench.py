@@ -120,6 +120,28 @@ def main():
                     libs[v].rxg_event_destroy(eng.ctx, a)
                     libs[v].rxg_event_destroy(eng.ctx, b)
                 rxg._lib = main_lib
+    if args.check and args.tx:
+        # every variant regenerates the checksums of a copy of batch 0 whose four checksum
+        # bytes were zeroed; the result must equal the synthesised batch byte for byte
+        for w, (bs, nbytes, tcb, live, nfr) in wls.items():
+            b = bs[0]
+            ref = b["arena"].download(np.uint8, b["arena_bytes"])
+            offs = b["off64"].download(np.uint32, nfr).astype(np.int64) * 64
+            lens = b["len"].download(np.uint16, nfr).astype(np.int64)
+            z = ref.copy()
+            for bp in (24, 25, 50, 51):
+                m = lens > bp
+                z[offs[m] + bp] = 0
+            for v, eng in engines.items():
+                rxg._lib = libs[v]
+                d = eng.to_device(z)
+                eng.tx_cksum_dev(d.ptr, b["off64"].ptr, b["len"].ptr, nfr)
+                eng.sync()
+                got = d.download(np.uint8, b["arena_bytes"])
+                d.free()
+                rxg._lib = main_lib
+                print(json.dumps({"check": w, "variant": v, "tx_bytes_equal": bool(np.array_equal(got, ref)),
+                                  "zeroed_differs": bool(not np.array_equal(z, ref))}), flush=True)
     if args.check and not args.tx:
         for w, (bs, nbytes, tcb, live, nfr) in wls.items():
             ref = None
