@@ -35,16 +35,16 @@ def main():
     dev = {}
     for k, p in orders.items():
         dev[k] = (eng.to_device(np.ascontiguousarray(off[p])), eng.to_device(np.ascontiguousarray(lens[p])))
-    out = eng.alloc(n * 16)
+    out = eng.alloc(n * 8)
     res = {k: [] for k in orders}
     for r in range(5):
         for k, (do, dl) in dev.items():
             evs = [(eng.event(), eng.event()) for _ in range(10)]
             for _ in range(2):
-                eng.rx_burst_dev(b["arena"].ptr, do.ptr, dl.ptr, n, out.ptr, rxg.REC16)
+                eng.rx_burst_dev(b["arena"].ptr, do.ptr, dl.ptr, n, out.ptr, rxg.REC8)
             for a, e in evs:
                 eng.record(a)
-                eng.rx_burst_dev(b["arena"].ptr, do.ptr, dl.ptr, n, out.ptr, rxg.REC16)
+                eng.rx_burst_dev(b["arena"].ptr, do.ptr, dl.ptr, n, out.ptr, rxg.REC8)
                 eng.record(e)
             eng.sync()
             res[k].append(float(np.median([eng.elapsed_ms(a, e) for a, e in evs])))
