@@ -41,7 +41,10 @@ TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.jso
                  ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r03/final/c3/traffic.json",
                  ("c2_64B_1flow", 1 << 20, 8): "profiles/r03/final/c2/traffic.json",
                  ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r03/final/c4/traffic.json",
-                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r03/final/c2multi/traffic.json"}
+                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r03/final/c2multi/traffic.json",
+                 # the 8(f) kernels over the headline's C3 batch (scripts/gpu_prof.sh tx3 / pg3)
+                 ("tx_generate_dev", 1 << 20, 8): "profiles/r03/final/tx3/traffic.json",
+                 ("payload_gather", 1 << 20, 8): "profiles/r03/final/pg3/traffic.json"}
 
 
 def traffic_of(name, n, rec):
@@ -353,7 +356,9 @@ def payload_leg(eng, wl, steps, warmup):
         k = float(np.mean(ms)) / 1e3
         alg = 2 * dl + (wl.rec + 16) * wl.n
         assert int(used.download(np.uint64, 1)[0]) == cap
+        tb = traffic_of("payload_gather", wl.n, wl.rec)[0] if wl.name == "c3_1500B_1Kflows" else None
         return {"payload_bytes": dl, "arena_bytes": cap, "record_bytes": wl.rec,
+                "traffic_bytes_per_launch": tb,
                 "kernels_us": round(k * 1e6, 2), "achieved_GBps": round(alg / k / 1e9, 1),
                 "roofline_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": alg}
@@ -378,7 +383,9 @@ def tx_leg(eng, wl, steps, warmup):
         eng.record(e)
     eng.sync()
     k = float(np.mean([eng.elapsed_ms(a, e) for a, e in evs])) / 1e3
+    tb = traffic_of("tx_generate_dev", wl.n, wl.rec)[0] if wl.name == "c3_1500B_1Kflows" else None
     return {"kernel_us": round(k * 1e6, 2), "mpps": round(wl.n / k / 1e6, 1),
+            "algorithmic_bytes_per_launch": wl.bytes_per_batch, "traffic_bytes_per_launch": tb,
             "achieved_GBps": round(wl.bytes_per_batch / k / 1e9, 1),
             "roofline_frac": round(wl.bytes_per_batch / k / 1e9 / HBM_PEAK_GBS, 4)}
 

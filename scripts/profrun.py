@@ -19,7 +19,7 @@ WL = {"c3": (1500, 1000, 0, 2), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3)}
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c3", choices=sorted(WL) + ["c2multi"])
+    ap.add_argument("--workload", default="c3", choices=sorted(WL) + ["c2multi", "tx3", "tx4", "pg3", "pg4"])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rec", type=int, default=16, choices=[8, 16, 48])
@@ -37,6 +37,29 @@ def main():
         for _ in range(args.iters):
             eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
         eng.sync()
+        return
+    if args.workload[:2] in ("tx", "pg"):
+        # bench.py tx_leg / payload_leg over the C3 ("3") or C4 ("4") batch: rxg_tx_cksum_dev
+        # in place (the batch's checksums are already the generated ones), or one rx burst then
+        # rxg_payload_gather_dev into an arena of exactly the burst's size
+        L, flows, mix, copies = WL["c3" if args.workload[2] == "3" else "c4"]
+        b = eng.synth(n=n, nflows=flows, len_a=L or 1500, mix=mix, seed=0x5EED0001)
+        eng.tcb_load(*rxg.synthetic_tcb_table(flows))
+        if args.workload[:2] == "tx":
+            for _ in range(args.iters):
+                eng.tx_cksum_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n)
+            eng.sync()
+            return
+        import numpy as np
+        out = eng.alloc(n * rec)
+        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, out.ptr, rec)
+        pl = (b["len"].download(np.uint16, n).astype(np.int64) - 54).clip(min=0)
+        cap = int(((pl + 15) // 16 * 16).sum())
+        arena, msgs, used = eng.alloc(cap), eng.alloc(n * 16), eng.alloc(8)
+        for _ in range(args.iters):
+            eng.payload_gather_dev(arena.ptr, cap, msgs.ptr, used.ptr)
+        eng.sync()
+        assert int(used.download(np.uint64, 1)[0]) == cap
         return
     L, flows, mix, copies = WL[args.workload]
     bs = [eng.synth(n=n, nflows=flows, len_a=L or 1500, mix=mix, seed=0x5EED0001 + 17 * c) for c in range(copies)]
