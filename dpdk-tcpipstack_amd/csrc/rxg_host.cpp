@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <thread>
 #include <unordered_map>
@@ -94,6 +95,7 @@ struct rxg_ctx {
     // waited for).
     hipEvent_t mirror_ev = nullptr;
     bool mirror_ev_set = false;
+    uint64_t table_writes = 0;  // mirror_ev recordings (device table writes) so far
     struct Reader {
         hipStream_t s;
         hipEvent_t e;
@@ -192,6 +194,24 @@ struct rxg_ctx {
     uint8_t *d_out = nullptr;
     uint8_t *h_out = nullptr;        // pinned records of zero-copy host bursts
     uint64_t zc_bytes = 64ull << 20; // host bursts up to this many staged bytes: zero-copy
+
+    // latency-mode server (rxg_server_*): a persistent kernel on its own
+    // stream, a mailbox and staging in coherent host memory
+    struct Server {
+        bool on = false;        // configured (the kernel may have exited idle: relaunched on demand)
+        bool launched = false;  // a kernel was launched since the last stream synchronisation
+        hipStream_t st = nullptr;
+        SrvMbox *mbox = nullptr;
+        SrvCtl *ctl = nullptr;
+        uint8_t *arena = nullptr;
+        uint32_t *off = nullptr;
+        uint16_t *len = nullptr;
+        uint8_t *out = nullptr;
+        uint32_t rec_kind = 0, blocks = 1, max_frames = 0;
+        uint64_t max_bytes = 0, idle_ticks = 0;
+        unsigned long long seq = 0;
+        uint64_t seen_writes = ~0ull;  // table_writes as of the last request served
+    } srv;
 };
 
 static constexpr size_t kCounterBytes = (size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS * sizeof(uint64_t);
@@ -313,6 +333,7 @@ extern "C" int rxg_fini(rxg_ctx *c)
 {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
+    (void)rxg_server_stop(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &r : c->readers)  // table readers still running on caller streams
         if (r.set) (void)hipEventSynchronize(r.e);
@@ -551,6 +572,7 @@ static int apply_patches(rxg_ctx *c, M &mirror)
     pb.set = true;
     HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
     c->mirror_ev_set = true;
+    ++c->table_writes;
     mirror.patches_taken();
     return 0;
 }
@@ -581,6 +603,7 @@ static int tcb_push(rxg_ctx *c)
         HIP_OK(hipStreamSynchronize(c->stream));
         HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
         c->mirror_ev_set = true;
+        ++c->table_writes;
     } else if ((rc = apply_patches(c, m))) {
         return rc;
     }
@@ -641,6 +664,7 @@ static int arp_sync(rxg_ctx *c)
         HIP_OK(hipStreamSynchronize(c->stream));
         HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
         c->mirror_ev_set = true;
+        ++c->table_writes;
     } else if ((rc = apply_patches(c, a))) {
         return rc;
     }
@@ -717,8 +741,9 @@ static void select_burst(rxg_ctx *c, uint32_t j)
 // kMaxBursts bursts.  The bursts are then replayed in order (rxg_rx_replay).
 static bool rec_kind_ok(uint32_t k) { return k == RXG_REC8 || k == RXG_REC16 || k == RXG_REC48; }
 
-static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
-                         void *stream, const char *who)
+// Validation, mirror sync and the replay bookkeeping of a burst set (launched or served).
+static int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
+                        const char *who)
 {
     // a rejected launch leaves nothing to replay: rxg_rx_replay refuses until a burst succeeds
     c->burst_ok = false;
@@ -761,6 +786,14 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
     c->launch_keys.clear();
     c->launch_listen.clear();
     c->launch_all = c->launch_pass2 = false;
+    return 0;
+}
+
+static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
+                         void *stream, const char *who)
+{
+    int rc = begin_bursts(c, frames, bursts, k, rec_kind, who);
+    if (rc) return rc;
     hipStream_t st = pick(c, stream);
     if ((rc = order_table_reader_before(c, st))) return rc;
     LaunchBurst lb[kMaxBursts];
@@ -803,6 +836,168 @@ extern "C" int rxg_rx_bursts_dev(rxg_ctx *c, const void *frames, const rxg_dev_b
     return launch_bursts(c, frames, bursts, k, rec_kind, stream, "rxg_rx_bursts_dev");
 }
 
+// ---------------------------------------------------------------- latency mode ---
+// (Re)launch the server kernel.  A previous kernel has left its loop (stop / idle) or was
+// never launched; its stream is synchronised before the mailbox and control words reset.
+static int srv_launch(rxg_ctx *c)
+{
+    rxg_ctx::Server &S = c->srv;
+    if (S.launched) {
+        HIP_OK(hipStreamSynchronize(S.st));
+        S.launched = false;
+    }
+    __atomic_store_n(&S.mbox->stop, 0ull, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&S.mbox->exited, 0ull, __ATOMIC_SEQ_CST);
+    SrvCtl init;
+    std::memset(&init, 0, sizeof init);
+    init.go = __atomic_load_n(&S.mbox->done, __ATOMIC_ACQUIRE);  // the workgroups wait past it
+    HIP_OK(hipMemcpyAsync(S.ctl, &init, sizeof init, hipMemcpyHostToDevice, S.st));
+    HIP_OK(hipStreamSynchronize(S.st));
+    LaunchServer L;
+    L.mbox = S.mbox;
+    L.ctl = S.ctl;
+    L.counters = c->counters;
+    L.idle_ticks = S.idle_ticks;
+    L.blocks = S.blocks;
+    L.mode = (int)S.rec_kind;
+    L.variant = c->variant;
+    HIP_OK(launch_server(L, S.st));
+    S.launched = true;
+    return 0;
+}
+
+// Post one request and wait for its `done`.  A kernel that exited idle before it saw the
+// request is relaunched; the new one starts from `done` and serves it.
+static int srv_post(rxg_ctx *c, const SrvReq &r)
+{
+    rxg_ctx::Server &S = c->srv;
+    int rc;
+    if ((!S.launched || __atomic_load_n(&S.mbox->exited, __ATOMIC_ACQUIRE)) && (rc = srv_launch(c))) return rc;
+    S.mbox->req = r;
+    const unsigned long long q = ++S.seq;
+    __atomic_store_n(&S.mbox->seq, q, __ATOMIC_SEQ_CST);  // the request's fields before seq
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spins = 1;; ++spins) {
+        if (__atomic_load_n(&S.mbox->done, __ATOMIC_ACQUIRE) == q) break;
+        __builtin_ia32_pause();
+        if ((spins & 1023u) == 0u) {
+            if (__atomic_load_n(&S.mbox->exited, __ATOMIC_ACQUIRE)) {
+                if (__atomic_load_n(&S.mbox->done, __ATOMIC_ACQUIRE) == q) break;
+                if ((rc = srv_launch(c))) return rc;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_SEQ_CST);
+                return fail(-ETIMEDOUT, "rxg_server: request %llu not served in 10 s", q);
+            }
+        }
+    }
+    return 0;
+}
+
+static void srv_free(rxg_ctx *c)
+{
+    rxg_ctx::Server &S = c->srv;
+    for (void *h : {(void *)S.mbox, (void *)S.arena, (void *)S.off, (void *)S.len, (void *)S.out})
+        if (h) (void)hipHostFree(h);
+    if (S.ctl) (void)hipFree(S.ctl);
+    if (S.st) (void)hipStreamDestroy(S.st);
+    S = rxg_ctx::Server{};
+}
+
+extern "C" int rxg_server_stop(rxg_ctx *c)
+{
+    if (!c) return fail(-EINVAL, "rxg_server_stop: ctx NULL");
+    if (!c->srv.on) return 0;
+    int rc = set_device(c);
+    if (rc) return rc;
+    rxg_ctx::Server &S = c->srv;
+    hipError_t e = hipSuccess;
+    if (S.launched) {
+        __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_SEQ_CST);
+        e = hipStreamSynchronize(S.st);
+    }
+    srv_free(c);
+    if (e != hipSuccess) return fail(-EIO, "rxg_server_stop: %s", hipGetErrorString(e));
+    return 0;
+}
+
+extern "C" int rxg_server_start(rxg_ctx *c, const rxg_server_config *cfg)
+{
+    if (!c || !cfg) return fail(-EINVAL, "rxg_server_start: NULL argument");
+    if (!rec_kind_ok(cfg->rec_kind)) return fail(-EINVAL, "rxg_server_start: rec_kind %u", cfg->rec_kind);
+    const uint32_t blocks = cfg->blocks ? cfg->blocks : 1u;
+    const uint32_t maxf = cfg->max_frames ? cfg->max_frames : 4096u;
+    if (blocks > 256u) return fail(-EINVAL, "rxg_server_start: %u workgroups (at most 256)", blocks);
+    if (maxf > (1u << 20)) return fail(-EINVAL, "rxg_server_start: max_frames %u (at most 2^20)", maxf);
+    int rc = rxg_server_stop(c);
+    if (rc) return rc;
+    if ((rc = set_device(c))) return rc;
+    rxg_ctx::Server &S = c->srv;
+    S.rec_kind = cfg->rec_kind;
+    S.blocks = blocks;
+    S.max_frames = maxf;
+    S.max_bytes = cfg->max_bytes ? cfg->max_bytes : (uint64_t)maxf * 2048u;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0)
+        khz = 100000;  // 100 MHz, the MI300-series constant clock
+    S.idle_ticks = (uint64_t)(cfg->idle_ms ? cfg->idle_ms : 1000u) * (uint64_t)khz;
+    const unsigned flags = hipHostMallocCoherent | hipHostMallocMapped;
+    bool ok = hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) == hipSuccess &&
+              hipHostMalloc((void **)&S.mbox, sizeof(SrvMbox), flags) == hipSuccess &&
+              hipHostMalloc((void **)&S.arena, S.max_bytes, flags) == hipSuccess &&
+              hipHostMalloc((void **)&S.off, (size_t)maxf * 4u, flags) == hipSuccess &&
+              hipHostMalloc((void **)&S.len, (size_t)maxf * 2u, flags) == hipSuccess &&
+              hipHostMalloc((void **)&S.out, (size_t)maxf * cfg->rec_kind, flags) == hipSuccess &&
+              hipMalloc((void **)&S.ctl, sizeof(SrvCtl)) == hipSuccess;
+    if (!ok) {
+        srv_free(c);
+        return fail(-ENOMEM, "rxg_server_start: mailbox / staging for %u frames", maxf);
+    }
+    std::memset(S.mbox, 0, sizeof(SrvMbox));
+    S.on = true;
+    if ((rc = srv_launch(c))) {
+        srv_free(c);
+        return rc;
+    }
+    return 0;
+}
+
+extern "C" int rxg_server_active(rxg_ctx *c) { return c && c->srv.on ? 1 : 0; }
+
+extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b)
+{
+    if (!c || !b) return fail(-EINVAL, "rxg_server_burst_dev: NULL argument");
+    if (!c->srv.on) return fail(-ENODEV, "rxg_server_burst_dev: no server (rxg_server_start)");
+    if (b->rec_kind != c->srv.rec_kind)
+        return fail(-EINVAL, "rxg_server_burst_dev: rec_kind %u, the server's is %u", b->rec_kind, c->srv.rec_kind);
+    if (b->n > c->srv.max_frames)
+        return fail(-EINVAL, "rxg_server_burst_dev: n=%u exceeds max_frames=%u", b->n, c->srv.max_frames);
+    if (b->n && (!b->frames || !b->off64 || !b->len || !b->out))
+        return fail(-EINVAL, "rxg_server_burst_dev: NULL device pointer");
+    const rxg_dev_burst one{b->off64, b->len, b->n, 0u, b->out};
+    int rc = begin_bursts(c, b->frames, &one, 1, b->rec_kind, "rxg_server_burst_dev");
+    if (rc) return rc;
+    // mirror writes queued on the context's stream land before the server reads the tables
+    if (c->mirror_ev_set) HIP_OK(hipEventSynchronize(c->mirror_ev));
+    if (b->n) {
+        SrvReq r;
+        std::memset(&r, 0, sizeof r);
+        r.frames = (const uint8_t *)b->frames;
+        r.off64 = b->off64;
+        r.len = b->len;
+        r.out = (uint8_t *)b->out;
+        r.n = b->n;
+        r.table = table_view(c);
+        // the CUs re-read device memory that changed: mirror tables written since the last
+        // request, or frames outside the server's own (uncached, coherent) staging
+        if (c->table_writes != c->srv.seen_writes || b->frames != c->srv.arena) r.flags |= kSrvInvalidate;
+        if ((rc = srv_post(c, r))) return rc;
+        c->srv.seen_writes = c->table_writes;
+    }
+    c->burst_ok = true;
+    return 0;
+}
+
 extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *stream)
 {
     if (!c || !b) return fail(-EINVAL, "rxg_tx_cksum_dev: NULL argument");
@@ -838,6 +1033,36 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
 {
     if (!c || (n && (!pkts || !out_host))) return fail(-EINVAL, "rxg_rx_burst: NULL argument");
     if (!rec_kind_ok(rec_kind)) return fail(-EINVAL, "rxg_rx_burst: rec_kind %u", rec_kind);
+    if (c->srv.on && rec_kind == c->srv.rec_kind && n && n <= c->srv.max_frames) {
+        // latency mode: packed into the server's coherent staging, served without a launch
+        rxg_ctx::Server &S = c->srv;
+        uint64_t slot = 0;
+        bool fits = true;
+        for (uint32_t i = 0; i < n && fits; ++i) {
+            const uint64_t need = (pkts[i].data_len + 63u) / 64u;
+            fits = (slot + need) * 64u <= S.max_bytes;
+            S.off[i] = (uint32_t)slot;
+            S.len[i] = pkts[i].data_len;
+            slot += need;
+        }
+        if (fits) {
+            for (uint32_t i = 0; i < n; ++i)
+                if (pkts[i].data_len)
+                    std::memcpy(S.arena + (uint64_t)S.off[i] * 64u,
+                                (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off, pkts[i].data_len);
+            rxg_dev_batch b;
+            b.frames = S.arena;
+            b.off64 = S.off;
+            b.len = S.len;
+            b.n = n;
+            b.rec_kind = rec_kind;
+            b.out = S.out;
+            int rc = rxg_server_burst_dev(c, &b);
+            if (rc) return rc;
+            std::memcpy(out_host, S.out, (size_t)n * rec_kind);
+            return 0;
+        }
+    }
     if (n > c->max_batch)
         return fail(-EINVAL, "rxg_rx_burst: n=%u exceeds max_batch=%u", n, c->max_batch);
     c->burst_ok = false;

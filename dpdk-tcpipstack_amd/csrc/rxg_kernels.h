@@ -57,6 +57,47 @@ struct LaunchPayload {
 };
 
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
+
+// Latency mode (rxg_server_*): a persistent set of workgroups that classifies one burst after
+// another.  The host posts a request in a mailbox of fine-grained (coherent) host memory and
+// spins on its `done`; workgroup 0 polls the mailbox and hands each request to the others
+// through `SrvCtl` in device memory.  No launch and no stream synchronisation per burst.
+struct SrvReq {
+    const uint8_t *frames;   // device-visible: HBM or mapped host memory
+    const uint32_t *off64;
+    const uint16_t *len;
+    uint8_t *out;            // records of the server's kind
+    uint32_t n;
+    uint32_t flags;          // kSrvInvalidate
+    DevTable table;          // the mirror as of the post
+};
+// SrvReq.flags: device memory the request reads may have changed since the last request
+// (mirror writes, caller-written frames): every workgroup's CU invalidates its L1 first
+constexpr uint32_t kSrvInvalidate = 1u;
+struct SrvMbox {                  // coherent host memory
+    unsigned long long seq;       // host: number of the request posted (release)
+    unsigned long long done;      // server: number of the last request finished (release)
+    unsigned long long stop;      // host: nonzero = exit
+    unsigned long long exited;    // server: nonzero once the kernel has left its loop
+    SrvReq req;
+};
+struct SrvCtl {                   // device memory
+    unsigned long long go;        // the request the workgroups run (kSrvStop: exit)
+    unsigned int fin;             // workgroups finished, all requests (monotonic)
+    unsigned int pad;
+    SrvReq req;
+};
+constexpr unsigned long long kSrvStop = ~0ull;
+struct LaunchServer {
+    SrvMbox *mbox;
+    SrvCtl *ctl;
+    unsigned long long *counters;
+    unsigned long long idle_ticks;  // wall-clock ticks without a request before the kernel exits
+    uint32_t blocks;
+    int mode;                       // record kind 8 / 16 / 48
+    int variant;                    // 0 = production; experiment variants (RXG_VARIANT)
+};
+hipError_t launch_server(const LaunchServer &L, hipStream_t st);
 // rxg_payload.hip: gather of the burst's candidate payloads (one launch + a memset)
 hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *tickets_used);
 uint32_t payload_blocks(uint32_t n);

@@ -1817,15 +1817,18 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
     return cont;
 }
 
-template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
-          bool DEFER = false, bool DTOP = true, int WPE = 0, bool DEEP = false, int TXD = 0>
 // TXD (tx, MODE 0): frames over 64 bytes (TXD 1), and 64-byte ones too (TXD 2), get their
 // first line rewritten by tx_flush, not in their round (TxQ).
 // WPE 0: no bound, except 3 waves per SIMD (at most 168 VGPRs) for rx kernels with the
 // software-pipelined rounds (experiment STRIP 32768), which would otherwise take 170 and drop to 2.
 // DEEP: runs of all-small slices prefetched two slices deep (small_step2); launch_rx picks it
 // for launches of at least kDeepSlicesPerWave slices per wave.
-__global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx_kernel(RxArgs a)
+// The body of workgroup blk of nblk (its waves are waves 4 blk .. 4 blk + 3 of 4 nblk dealing
+// the launch's slices).  rx_kernel (one launch per batch) and rx_server (a persistent set of
+// workgroups serving one burst after another) run it.
+template <int MODE, int CMASK, bool NT, int STRIP, bool SEL, int RS16, bool MULTI, bool DEFER, bool DTOP, bool DEEP,
+          int TXD>
+__device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
 {
     static_assert(!DEFER || MODE == 8 || MODE == 16, "deferred phase B: REC8 / REC16 only");
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -1846,8 +1849,8 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
     __shared__ uint2 s_txq[TXD ? 4 : 1][TXD ? kTxqCap : 1];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const uint32_t wave = blockIdx.x * 4u + (uint32_t)wid;
-    const uint32_t nwaves = gridDim.x * 4u;
+    const uint32_t wave = blk * 4u + (uint32_t)wid;
+    const uint32_t nwaves = nblk * 4u;
 
     WaveCounters wc;
 #pragma unroll
@@ -2059,8 +2062,161 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
         const int k = threadIdx.x;
         const unsigned long long v = s_cnt[0][k] + s_cnt[1][k] + s_cnt[2][k] + s_cnt[3][k];
         // replica row per workgroup (rxg.h RXG_COUNTER_ROWS): 32 adders per line, not 2048
-        if (v) atomicAdd(&a.counters[(blockIdx.x % kKernelCounterRows) * RXG_NCOUNTERS + k], v);
+        if (v) atomicAdd(&a.counters[(blk % kKernelCounterRows) * RXG_NCOUNTERS + k], v);
     }
+}
+
+template <int MODE, int CMASK, bool NT, int STRIP = 0, bool SEL = false, int RS16 = 11, bool MULTI = false,
+          bool DEFER = false, bool DTOP = true, int WPE = 0, bool DEEP = false, int TXD = 0>
+__global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx_kernel(RxArgs a)
+{
+    rx_body<MODE, CMASK, NT, STRIP, SEL, RS16, MULTI, DEFER, DTOP, DEEP, TXD>(a, blockIdx.x, gridDim.x);
+}
+
+// ------------------------------------------------------------- latency-mode server ---
+// rx_server: the same workgroup body as rx_kernel<MODE> (production form, one burst), run
+// once per request by a persistent grid (rxg_server_*).  Thread 0 of
+// workgroup 0 polls the host mailbox (system-scope acquire loads, s_sleep between polls).  A
+// request of P <= gridDim workgroups' worth of slices (4 slices per workgroup, one per wave,
+// then round-robin) runs on workgroups 0 .. P-1: when P > 1, workgroup 0 forwards it through
+// SrvCtl (agent-scope release / acquire); every participant classifies its slices, makes its
+// record stores visible, and the last to finish (a counter reset for the next request)
+// publishes `done`.  Exit: `stop`, or no request for idle_ticks of the constant-rate wall
+// clock (the host relaunches on its next burst), so a server whose process is gone ends by
+// itself.  STRIP (experiment builds): the rx body's form (32768 = pipelined rounds).
+struct SrvArgs {
+    SrvMbox *mbox;
+    SrvCtl *ctl;
+    unsigned long long *counters;
+    unsigned long long idle_ticks;
+};
+
+__device__ __forceinline__ unsigned long long srv_load(const unsigned long long *p, int scope)
+{
+    return scope == __HIP_MEMORY_SCOPE_SYSTEM ? __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)
+                                              : __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// workgroups a request of n frames runs on
+__device__ __forceinline__ uint32_t srv_participants(uint32_t n)
+{
+    const uint32_t nsl = (n + 63u) / 64u;
+    return max(1u, min(gridDim.x, (nsl + 3u) / 4u));
+}
+
+template <int MODE, int STRIP = 0>
+__global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArgs sa)
+{
+    __shared__ SrvReq s_req;
+    __shared__ unsigned long long s_go;
+    unsigned long long last = 0ull;  // thread 0: the last request this workgroup saw
+    if (threadIdx.x == 0) last = srv_load(&sa.mbox->done, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (;;) {
+        if (threadIdx.x == 0) {
+            unsigned long long go;
+            if (blockIdx.x == 0) {
+                const long long t0 = wall_clock64();
+                for (;;) {
+                    if (srv_load(&sa.mbox->stop, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) {
+                        go = kSrvStop;
+                        break;
+                    }
+                    const unsigned long long q = srv_load(&sa.mbox->seq, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (q != last) {
+                        go = q;
+                        break;
+                    }
+                    if ((unsigned long long)(wall_clock64() - t0) > sa.idle_ticks) {
+                        go = kSrvStop;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+                if (go != kSrvStop) s_req = sa.mbox->req;  // ordered after the acquire of seq
+                // the others hear of a request only when they take part in it (and of stop)
+                if (gridDim.x > 1 && (go == kSrvStop || srv_participants(s_req.n) > 1u)) {
+                    if (go != kSrvStop) sa.ctl->req = s_req;
+                    // release (MI355X_MICROARCH.md: the wait after the write-back, by hand)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&sa.ctl->go, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                for (;;) {
+                    go = srv_load(&sa.ctl->go, __HIP_MEMORY_SCOPE_AGENT);
+                    if (go != last) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (go != kSrvStop) s_req = sa.ctl->req;
+            }
+            s_go = go;
+            last = go;
+        }
+        __syncthreads();
+        const unsigned long long go = s_go;
+        if (go == kSrvStop) break;
+        const uint32_t P = srv_participants(s_req.n);
+        if (blockIdx.x >= P) {  // published for the first P workgroups of a larger grid
+            __syncthreads();
+            continue;
+        }
+        if (s_req.flags & kSrvInvalidate) {
+            // device-memory inputs (the mirror tables after a write, frames the caller rewrote)
+            // changed since this CU last read them: one agent-scope acquire per CU, waited
+            // for before any wave loads (MI355X_MICROARCH.md, inter-workgroup visibility)
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+        }
+        RxArgs a;
+        a.frames = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)s_req.frames));
+        a.sel = nullptr;
+        a.nbursts = 1u;
+        a.t.buckets = reinterpret_cast<const uint4 *>(uniform64((uint64_t)s_req.table.buckets));
+        a.t.listen = reinterpret_cast<const int32_t *>(uniform64((uint64_t)s_req.table.listen));
+        a.t.arp = reinterpret_cast<const uint4 *>(uniform64((uint64_t)s_req.table.arp));
+        a.t.bucket_mask = uniform(s_req.table.bucket_mask);
+        a.t.ntcb = (int32_t)uniform((uint32_t)s_req.table.ntcb);
+        a.t.min_null = (int32_t)uniform((uint32_t)s_req.table.min_null);
+        a.t.arp_mask = uniform(s_req.table.arp_mask);
+        a.t.arp_flags = uniform(s_req.table.arp_flags);
+        a.counters = sa.counters;
+        a.b[0].off64 = reinterpret_cast<const uint32_t *>(uniform64((uint64_t)s_req.off64));
+        a.b[0].len = reinterpret_cast<const uint16_t *>(uniform64((uint64_t)s_req.len));
+        a.b[0].out = reinterpret_cast<uint8_t *>(uniform64((uint64_t)s_req.out));
+        a.b[0].n = uniform(s_req.n);
+        a.b[0].slice0 = 0u;
+        a.nslices = (a.b[0].n + 63u) / 64u;
+        rx_body<MODE, 0xFF, true, STRIP, false, 11, false, false, true, false, 0>(a, blockIdx.x, P);
+        // this wave's records have reached their memory before `done`
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            bool lastp = true;
+            if (P > 1u) {
+                lastp = atomicAdd(&sa.ctl->fin, 1u) + 1u == P;
+                if (lastp) atomicExch(&sa.ctl->fin, 0u);  // before `done`: the next request counts from 0
+            }
+            if (lastp) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&sa.mbox->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        __syncthreads();  // s_req and s_go are rewritten by the next request
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&sa.mbox->exited, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------ synthetic frames ---
@@ -2431,6 +2587,28 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         else
 #endif
             hipLaunchKernelGGL((rx_kernel<0, 0xFF, true>), dim3(blocks), dim3(256), 0, st, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_server(const LaunchServer &L, hipStream_t st)
+{
+    SrvArgs sa{L.mbox, L.ctl, L.counters, L.idle_ticks};
+    const dim3 g(L.blocks ? L.blocks : 1u), b(256);
+    // the streaming classes' rounds software-pipelined (STRIP 32768): a served burst's frame
+    // reads are latency-bound (one wave per 64 frames, often over PCIe), and the second
+    // round in flight took 32 x 1500 B bursts from 25.6-27.6 to 22.2-23.2 us
+#ifdef RXG_EXPERIMENTS
+    if (L.variant == 78 && L.mode == 8) {  // the unpipelined body
+        hipLaunchKernelGGL((rx_server<8, 0>), g, b, 0, st, sa);
+        return hipGetLastError();
+    }
+#endif
+    switch (L.mode) {
+    case 8: hipLaunchKernelGGL((rx_server<8, 32768>), g, b, 0, st, sa); break;
+    case 16: hipLaunchKernelGGL((rx_server<16, 32768>), g, b, 0, st, sa); break;
+    case 48: hipLaunchKernelGGL((rx_server<48, 32768>), g, b, 0, st, sa); break;
+    default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

@@ -126,6 +126,12 @@ class DevBatch(C.Structure):
                 ("n", C.c_uint32), ("rec_kind", C.c_uint32), ("out", C.c_void_p)]
 
 
+class ServerConfig(C.Structure):
+    """rxg_server_config: latency mode (rxg_server_start)."""
+    _fields_ = [("rec_kind", C.c_uint32), ("blocks", C.c_uint32), ("max_frames", C.c_uint32),
+                ("max_bytes", C.c_uint32), ("idle_ms", C.c_uint32), ("pad", C.c_uint32)]
+
+
 class DevBurst(C.Structure):
     """rxg_dev_burst: one burst of a multi-burst launch (rxg_rx_bursts_dev)."""
     _fields_ = [("off64", C.c_void_p), ("len", C.c_void_p), ("n", C.c_uint32), ("pad", C.c_uint32),
@@ -229,6 +235,10 @@ def load_library(path: str = LIB_PATH):
         "rxg_rx_bursts_dev": (C.c_int, [vp, vp, vp, u32, u32, vp]),
         "rxg_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
         "rxg_tx_cksum_dev": (C.c_int, [vp, C.POINTER(DevTxBatch), vp]),
+        "rxg_server_start": (C.c_int, [vp, C.POINTER(ServerConfig)]),
+        "rxg_server_stop": (C.c_int, [vp]),
+        "rxg_server_active": (C.c_int, [vp]),
+        "rxg_server_burst_dev": (C.c_int, [vp, C.POINTER(DevBatch)]),
         "rxg_counters_reset": (C.c_int, [vp, vp]),
         "rxg_counters_read": (C.c_int, [vp, vp]),
         "rxg_counters_dev": (vp, [vp]),
@@ -282,6 +292,8 @@ def load_library(path: str = LIB_PATH):
         "rxg_group_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if path != LIB_PATH and not hasattr(lib, name):
+            continue  # an older build loaded for an A/B (scripts/kbench.py): its own entry points only
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -557,6 +569,23 @@ class Engine:
         arr = (DevBurst * max(len(bursts), 1))(*[DevBurst(o, l, n, 0, out) for o, l, n, out in bursts])
         _check(_lib.rxg_rx_bursts_dev(self.ctx, frames, arr, len(bursts), rec_kind, stream),
                "rxg_rx_bursts_dev")
+
+    # --- latency mode (rxg_server_*): a persistent kernel serves small bursts
+    def server_start(self, rec_kind: int = REC8, blocks: int = 1, max_frames: int = 4096,
+                     max_bytes: int = 0, idle_ms: int = 1000):
+        cfg = ServerConfig(rec_kind, blocks, max_frames, max_bytes, idle_ms, 0)
+        _check(_lib.rxg_server_start(self.ctx, C.byref(cfg)), "rxg_server_start")
+
+    def server_stop(self):
+        _check(_lib.rxg_server_stop(self.ctx), "rxg_server_stop")
+
+    def server_active(self) -> bool:
+        return bool(_lib.rxg_server_active(self.ctx))
+
+    def server_burst_dev(self, frames: int, off64: int, lens: int, n: int, out: int, rec_kind: int = REC8):
+        """Synchronous: the records are at `out` on return."""
+        b = DevBatch(frames, off64, lens, n, rec_kind, out)
+        _check(_lib.rxg_server_burst_dev(self.ctx, C.byref(b)), "rxg_server_burst_dev")
 
     def tx_cksum_dev(self, frames: int, off64: int, lens: int, n: int, stream=None):
         b = DevTxBatch(frames, off64, lens, n, 0)

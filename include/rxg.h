@@ -369,6 +369,35 @@ typedef struct rxg_pkt_view {
 int rxg_rx_burst(rxg_ctx *ctx, const rxg_pkt_view *pkts, uint32_t n, uint32_t rec_kind,
                  void *out_host);
 
+/* Latency mode for the reference's own burst size (MAX_PKT_BURST = 32, main.c:116; the loop
+   main.c:391-399 runs once per rte_eth_rx_burst).  A launched burst pays a kernel launch
+   and a stream synchronisation (~20 us for 32 frames); the server is a persistent set of
+   `blocks` workgroups of the same kernel body that polls a mailbox in coherent host memory,
+   so a burst costs the PCIe round trips of its frames and records.  While the server runs,
+   rxg_rx_burst sends bursts of up to max_frames frames (max_bytes staged bytes) and of
+   record kind rec_kind through it (packed into the server's own coherent staging), and
+   rxg_server_burst_dev serves device-visible batches.  Records, counters, replay and
+   payload gather are those of the launched path.  The server exits by itself after idle_ms
+   without a burst (and is relaunched by the next one), so it never outlives its process for
+   long.  Calls from the context's rx thread only.  Returns 0 or a negative errno. */
+typedef struct rxg_server_config {
+    uint32_t rec_kind;    /* RXG_REC8 / RXG_REC16 / RXG_REC48 */
+    uint32_t blocks;      /* workgroups (4 waves each); 0 = 1 */
+    uint32_t max_frames;  /* largest burst served; 0 = 4096 */
+    uint32_t max_bytes;   /* staging bytes for host bursts; 0 = max_frames * 2048 */
+    uint32_t idle_ms;     /* exit after this long without a burst; 0 = 1000 */
+    uint32_t pad;
+} rxg_server_config;
+int rxg_server_start(rxg_ctx *ctx, const rxg_server_config *cfg);
+/* Stops the server and waits for its kernel to end; 0 if none runs. */
+int rxg_server_stop(rxg_ctx *ctx);
+/* 1 if a server is configured (running or idle-exited, relaunched on demand), else 0. */
+int rxg_server_active(rxg_ctx *ctx);
+/* Classify a device-visible batch (HBM or mapped host memory) through the server:
+   b->rec_kind must be the server's, b->n <= max_frames.  Synchronous: returns once the
+   records are written at b->out.  -ENODEV without a server. */
+int rxg_server_burst_dev(rxg_ctx *ctx, const rxg_dev_batch *b);
+
 /* ------------------------------------------------------------------------- */
 /* Transmit checksum generate: what ip_out computes (ip.c:97-118) for a batch  */
 /* of frames whose Ethernet/IPv4/TCP headers the host has filled.  Writes      */

@@ -14,8 +14,11 @@ if(0)) and "verify" (with the rx checksum rxg computes).  The reference handles 
 at a time, so its burst time is n x its per-packet time, measured on a bounded sample of the
 same frames after one pass has taught its ARP list the sample's sources.
 
+Latency mode (round 3): the same bursts through the persistent server (rxg_server_start;
+bursts up to 4 096 frames, 1 and 4 workgroups) are timed beside the launched form.
+
 Prints one JSON line per (frame size, flows) and a summary line with the crossover burst
-sizes.  Runs on the GPU box (host cores + one GPU): python scripts/crossover.py
+sizes.  Runs on the GPU box (host cores + one GPU): python scripts/crossover.py [--no-cpu]
 """
 import ctypes as C
 import json
@@ -66,6 +69,7 @@ def cpu_pkt_us(arena, off, lens, tcb, live, opt, shipped, budget=1.0):
 
 
 def main():
+    no_cpu = "--no-cpu" in sys.argv
     nmax = max(BURSTS)
     eng = rxg.Engine(0, max_batch=nmax, max_bytes=nmax * 1536)
     lib = rxg.load_library()
@@ -87,19 +91,27 @@ def main():
             views = (rxg.PktView * nmax)(*[rxg.PktView(base + int(o) * 64, 0, int(ln), 0) for o, ln in zip(off, lens)])
             ptrs = (C.c_void_p * nmax)(*[base + int(o) * 64 for o in off])
             g = {n: round(rxg_burst_us(eng, lib, views, ptrs, out, n), 1) for n in BURSTS}
+            srv = {}
+            for blocks in (1, 4):
+                eng.server_start(rxg.REC8, blocks=blocks, max_frames=4096)
+                srv[blocks] = {n: round(rxg_burst_us(eng, lib, views, ptrs, out, n), 1) for n in BURSTS if n <= 4096}
+                eng.server_stop()
             sample = 4096 if flows < 65536 else 1024
             cpu = {}
-            for opt in ("O0", "O2"):
+            for opt in (() if no_cpu else ("O0", "O2")):
                 for shipped in (True, False):
                     cpu[f"{opt}_{'shipped' if shipped else 'verify'}"] = round(
                         cpu_pkt_us(arena, off[:sample], lens[:sample], tcb, live, opt, shipped), 4)
             row = {"frame_bytes": size, "flows": flows, "tcbs": flows + 1,
                    "rxg_burst_plus_replay_us": g,
+                   "server_burst_plus_replay_us": {f"{b}wg": v for b, v in srv.items()},
                    "rxg_mpps": {n: round(n / g[n], 3) for n in BURSTS},
                    "cpu_us_per_packet": cpu,
                    "cpu_mpps": {k: round(1.0 / v, 4) for k, v in cpu.items()},
                    # smallest measured burst at which rxg's burst time is below the CPU's n x per-packet
                    "crossover_burst": {k: next((n for n in BURSTS if g[n] < n * v), None) for k, v in cpu.items()},
+                   "crossover_burst_server": {k: next((n for n in BURSTS if min(g[n], *(s.get(n, 1e9) for s in srv.values())) < n * v), None)
+                                              for k, v in cpu.items()},
                    "cpu_sample": f"first {sample} frames, ARP list learned from them, 1 core"}
             rows.append(row)
             print(json.dumps(row), flush=True)

@@ -1,0 +1,185 @@
+"""GPU: latency mode (include/rxg.h rxg_server_*).  A persistent kernel serves bursts posted
+through a host-coherent mailbox; its records, counters and replay must equal the launched
+path's and the oracle's, burst after burst (fresh frame content each time: no stale reads of
+host memory), across mirror writes, idle exits and restarts."""
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+import pktgen
+import rxg
+import test_gpu_replay
+from test_gpu_parity import assert_records_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def srv_engine():
+    eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20)
+    yield eng
+    eng.close()
+
+
+def _upload(eng, arena, off, lens):
+    return eng.to_device(arena), eng.to_device(off.astype(np.uint32)), eng.to_device(lens.astype(np.uint16))
+
+
+@pytest.mark.parametrize("blocks", [1, 3])
+def test_server_bursts_equal_launched(srv_engine, blocks):
+    """Sub-bursts of every shape (1 .. 4096 frames, partial slices) of one device batch: the
+    served records equal one launched burst's, byte for byte, and so do the counters."""
+    eng = srv_engine
+    rows, frames = pktgen.parity_set(seed=71 + blocks, n=6000)
+    arena, off, lens = pktgen.pack_arena(frames)
+    tcb, live = pktgen.table_arrays(rows)
+    eng.tcb_load(tcb, live)
+    n = len(lens)
+    d_arena, d_off, d_len = _upload(eng, arena, off, lens)
+    ref = eng.alloc(n * 16)
+    out = eng.alloc(n * 16)
+    try:
+        eng.counters_reset()
+        eng.rx_burst_dev(d_arena.ptr, d_off.ptr, d_len.ptr, n, ref.ptr, rxg.REC16)
+        eng.sync()
+        exp_cnt = eng.counters()
+        exp = ref.download(np.uint8, n * 16)
+        eng.server_start(rxg.REC16, blocks=blocks, max_frames=4096)
+        assert eng.server_active()
+        eng.counters_reset()
+        i = 0
+        for k in [1, 32, 63, 64, 65, 100, 255, 1000, 4096, 3, 32, 32, 31, 257] * 2:
+            k = min(k, n - i)
+            if k == 0:
+                break
+            eng.server_burst_dev(d_arena.ptr, d_off.ptr + 4 * i, d_len.ptr + 2 * i, k, out.ptr + 16 * i, rxg.REC16)
+            i += k
+        got = out.download(np.uint8, i * 16)
+        assert got.tobytes() == exp[: i * 16].tobytes()
+        if i == n:
+            assert eng.counters().tolist() == exp_cnt.tolist()
+        eng.server_stop()
+        assert not eng.server_active()
+    finally:
+        for d in (d_arena, d_off, d_len, ref, out):
+            d.free()
+
+
+@pytest.mark.parametrize("rec", [rxg.REC8, rxg.REC16, rxg.REC48])
+def test_server_host_bursts_equal_launched_and_oracle(srv_engine, rec):
+    """rxg_rx_burst through the server: 200 consecutive bursts of the reference's size class
+    (1..64 frames, fresh content every burst) equal the same bursts launched, and (REC48,
+    every field) the oracle."""
+    eng = srv_engine
+    rows, frames = pktgen.parity_set(seed=90 + rec, n=4000)
+    tcb, live = pktgen.table_arrays(rows)
+    eng.tcb_load(tcb, live)
+    rng = np.random.default_rng(rec)
+    bursts, i = [], 0
+    for _ in range(200):
+        k = int(rng.integers(1, 65))
+        bursts.append(frames[i:i + k])
+        i += k
+    eng.server_start(rec, max_frames=256)
+    try:
+        served = [eng.rx_burst(b, rec) for b in bursts]
+    finally:
+        eng.server_stop()
+    for b, got in zip(bursts, served):
+        assert eng.rx_burst(b, rec).tobytes() == got.tobytes()
+        if rec == rxg.REC48:
+            arena, off, lens = pktgen.pack_arena(b)
+            exp, _ = oracle.rx_batch(arena, off, lens, tcb, live)
+            assert_records_equal(got, exp, b)
+
+
+@pytest.mark.parametrize("blocks", [1, 3])
+def test_server_sees_mirror_writes(srv_engine, blocks):
+    """tcbs[] writes between served bursts (upsert, remove, set_state) are on the device
+    before the next burst reads the table: each served burst equals the oracle on the table
+    as it stands."""
+    eng = srv_engine
+    rows, frames = pktgen.parity_set(seed=5, n=1024, nflows=64)
+    tcb, live = pktgen.table_arrays(rows)
+    eng.tcb_load(tcb, live)
+    eng.server_start(rxg.REC48, blocks=blocks, max_frames=512)
+    rng = np.random.default_rng(5 + blocks)
+    try:
+        for step in range(30):
+            idx = int(rng.integers(1, len(tcb)))
+            if step % 3 == 0:
+                live[idx] = 0
+                eng.tcb_remove(idx)
+            elif step % 3 == 1 and live[idx]:
+                st = rxg.TCP_ESTABLISHED if tcb["state"][idx] != rxg.TCP_ESTABLISHED else rxg.LISTENING
+                tcb["state"][idx] = st
+                eng.tcb_set_state(idx, st)
+            else:
+                live[idx] = 1
+                t = tcb[idx]
+                eng.tcb_upsert(idx, int(t["dport"]), int(t["sport"]), int(t["ipv4_dst"]), int(t["ipv4_src"]),
+                               int(t["state"]), int(t["identifier"]))
+            fr = frames[step * 32: step * 32 + 32]
+            got = eng.rx_burst(fr, rxg.REC48)
+            arena, off, lens = pktgen.pack_arena(fr)
+            exp, _ = oracle.rx_batch(arena, off, lens, tcb, live)
+            assert_records_equal(got, exp, fr)
+    finally:
+        eng.server_stop()
+
+
+def test_server_idle_exit_and_relaunch(srv_engine):
+    """A server idle for longer than idle_ms exits; the next burst relaunches it.  Stop and
+    start again; a context closed with a running server stops it."""
+    eng = srv_engine
+    rows, frames = pktgen.parity_set(seed=11, n=256)
+    tcb, live = pktgen.table_arrays(rows)
+    eng.tcb_load(tcb, live)
+    arena, off, lens = pktgen.pack_arena(frames[:40])
+    exp = eng.rx_arena(arena, off, lens, rxg.REC16)
+    eng.server_start(rxg.REC16, max_frames=64, idle_ms=30)
+    for _ in range(3):
+        assert eng.rx_burst(frames[:40], rxg.REC16).tobytes() == exp.tobytes()
+        time.sleep(0.15)  # the kernel exits idle
+        assert eng.rx_burst(frames[:40], rxg.REC16).tobytes() == exp.tobytes()
+    eng.server_stop()
+    eng.server_start(rxg.REC16, max_frames=64)
+    assert eng.rx_burst(frames[:40], rxg.REC16).tobytes() == exp.tobytes()
+    # too large for the server: launched as before
+    assert eng.rx_burst(frames[:200], rxg.REC16).shape[0] == 200
+    other = rxg.Engine(device=0, max_batch=256, max_bytes=1 << 20)
+    other.server_start(rxg.REC8, max_frames=64)
+    other.close()  # stops its server
+
+
+def test_server_rejects_bad_requests(srv_engine):
+    eng = srv_engine
+    lib = rxg.load_library()
+    import ctypes as C
+    b = rxg.DevBatch(None, None, None, 1, rxg.REC8, None)
+    assert lib.rxg_server_burst_dev(eng.ctx, C.byref(b)) < 0  # no server
+    eng.server_start(rxg.REC8, max_frames=64)
+    try:
+        b = rxg.DevBatch(None, None, None, 65, rxg.REC8, None)
+        assert lib.rxg_server_burst_dev(eng.ctx, C.byref(b)) < 0  # too many
+        b = rxg.DevBatch(None, None, None, 1, rxg.REC16, None)
+        assert lib.rxg_server_burst_dev(eng.ctx, C.byref(b)) < 0  # wrong kind
+        b = rxg.DevBatch(None, None, None, 1, rxg.REC8, None)
+        assert lib.rxg_server_burst_dev(eng.ctx, C.byref(b)) < 0  # NULL pointers
+        cfg = rxg.ServerConfig(7, 1, 64, 0, 0, 0)
+        assert lib.rxg_server_start(eng.ctx, C.byref(cfg)) < 0
+    finally:
+        eng.server_stop()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_server_replay_sequential_equivalence(srv_engine, seed):
+    """The replay test of test_gpu_replay (in-burst SYN/FIN writes re-classified) with the
+    burst served instead of launched."""
+    srv_engine.server_start(rxg.REC16, max_frames=4096)
+    try:
+        test_gpu_replay.test_replay_sequential_equivalence(srv_engine, seed)
+    finally:
+        srv_engine.server_stop()
