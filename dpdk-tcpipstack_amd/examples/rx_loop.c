@@ -160,6 +160,17 @@ int main(int argc, char **argv)
         free(live);
     }
 
+    /* RX_LOOP_SERVER=1: the latency mode (rxg.h rxg_server_start), as INTEGRATION.md §2
+       starts it for the reference's MAX_PKT_BURST loop; the loop below is unchanged */
+    const char *srv = getenv("RX_LOOP_SERVER");
+    if (srv && strcmp(srv, "1") == 0) {
+        rxg_server_config sc = {RXG_REC8, 4u, burst, 0u, 0u, 0u};
+        if (rxg_server_start(g_rxg, &sc) != 0) {
+            fprintf(stderr, "rxg_server_start: %s\n", rxg_last_error());
+            return 3;
+        }
+    }
+
     g_out = calloc(n, sizeof *g_out);
     for (uint32_t i = 0; i < n; ++i) g_out[i].tcb_idx = -1;
     rxg_pkt_view *views = calloc(burst, sizeof *views);

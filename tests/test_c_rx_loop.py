@@ -60,15 +60,18 @@ def test_c_loop_builds_and_fails_loudly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("burst", [1, 32, 256])
-def test_c_loop_equals_sequential_reference(tmp_path, burst):
+@pytest.mark.parametrize("burst,server", [(1, False), (32, False), (256, False), (1, True), (32, True), (256, True)])
+def test_c_loop_equals_sequential_reference(tmp_path, burst, server):
+    """server: the same loop in latency mode (rxg_server_start, RX_LOOP_SERVER=1)."""
     from test_gpu_replay import scenario, sequential_reference
     import rxg
     rows, frames = scenario(7, n=600 if burst == 1 else 1500)
     exp, _, erows = sequential_reference(rows, frames)
     inp, outp = tmp_path / "in.bin", tmp_path / "out.bin"
     _write_input(inp, rows, frames)
-    r = subprocess.run([_exe(), str(inp), str(outp), str(burst)], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, RX_LOOP_SERVER="1" if server else "0")
+    r = subprocess.run([_exe(), str(inp), str(outp), str(burst)], capture_output=True, text=True, timeout=300,
+                       env=env)
     assert r.returncode == 0, r.stderr
     out, got_rows = _read_output(outp, len(frames))
     for i, (v, idx, st) in enumerate(exp):
