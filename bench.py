@@ -415,6 +415,57 @@ def replay_churn_leg():
     return out
 
 
+def small_burst_leg(gpu, n=32, seconds=0.3):
+    """SURVEY.md 8(a) A1 at the reference's own burst size (MAX_PKT_BURST = 32, main.c:116):
+    host frames through rxg_rx_burst + rxg_rx_replay (empty handlers), median microseconds per
+    burst, launched and through the latency-mode server (rxg_server_start),
+    64 B and 1 500 B frames, 1 000 flows, 8-byte records."""
+    import ctypes as C
+    e = rxg.Engine(device=gpu, max_batch=4096, max_bytes=4096 * 1536)
+    lib = rxg.load_library()
+    out = np.zeros(n, dtype=rxg.REC8_DTYPE)
+    ops = rxg.HandoffOps()
+    res = {}
+    try:
+        for size in (64, 1500):
+            b = e.synth(n=n, nflows=1000, len_a=size, seed=4242)
+            e.sync()
+            off = b["off64"].download(np.uint32, n)
+            lens = b["len"].download(np.uint16, n)
+            arena = b["arena"].download(np.uint8, b["arena_bytes"])
+            for v in b.values():
+                if isinstance(v, rxg.DevArray):
+                    v.free()
+            tcb, live = rxg.synthetic_tcb_table(1000)
+            e.tcb_load(tcb, live)
+            base = arena.ctypes.data
+            views = (rxg.PktView * n)(*[rxg.PktView(base + int(o) * 64, 0, int(ln), 0) for o, ln in zip(off, lens)])
+            ptrs = (C.c_void_p * n)(*[base + int(o) * 64 for o in off])
+
+            def one():
+                t = time.perf_counter()
+                assert lib.rxg_rx_burst(e.ctx, views, n, rxg.REC8, out.ctypes.data) == 0
+                assert lib.rxg_rx_replay(e.ctx, C.byref(ops), ptrs, ptrs, out.ctypes.data, n, rxg.REC8) == 0
+                return time.perf_counter() - t
+
+            def median_us():
+                for _ in range(5):
+                    one()
+                lat, t0 = [], time.perf_counter()
+                while time.perf_counter() - t0 < seconds or len(lat) < 20:
+                    lat.append(one())
+                return round(float(np.median(lat)) * 1e6, 2)
+            launched = median_us()
+            e.server_start(rxg.REC8, blocks=4, max_frames=4096)
+            served = median_us()
+            e.server_stop()
+            res[f"{size}B_x{n}"] = {"launched_us": launched, "served_us": served,
+                                    "served_mpps": round(n / served, 3)}
+    finally:
+        e.close()
+    return res
+
+
 def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
     """The oracle's faithful restatement of the reference rx path (port), on one host
     core, over a bounded sample of the same workload (first sample_n frames)."""
@@ -596,6 +647,7 @@ def main():
                                                  seed)
         if rank == 0:
             legs["replay_churn"] = replay_churn_leg()
+            legs["small_burst_latency"] = small_burst_leg(gpu)
         eng.tcb_load(tcb, live)
 
     # The reference rx path is one lcore (main.c:366-369): its baseline is a host figure,
