@@ -115,6 +115,34 @@ def test_group_and_null_arguments_fail_loudly():
     assert lib.rxg_host_register(None, None, 0, C.byref(d)) == -22
     assert lib.rxg_tcb_post(None, None) == -22
     assert lib.rxg_rx_burst(None, None, 0, 16, None) == -22
+    # latency mode (rxg_server_*): no context
+    cfg = rxg.ServerConfig(rxg.REC8, 1, 32, 0, 0, 0)
+    assert lib.rxg_server_start(None, C.byref(cfg)) == -22
+    assert lib.rxg_server_stop(None) == -22
+    assert lib.rxg_server_active(None) == 0
+    assert lib.rxg_server_burst_dev(None, None) == -22
+
+
+def test_server_config_layout_matches_header():
+    import ctypes as C
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "rxg.h"
+int main(void) {
+  printf("%zu %zu %zu\n", sizeof(rxg_server_config), offsetof(rxg_server_config, max_bytes),
+         offsetof(rxg_server_config, idle_ms));
+  return 0;
+}'''
+    tmp = os.path.join(ROOT, "build_abi_probe")
+    os.makedirs(tmp, exist_ok=True)
+    with open(os.path.join(tmp, "srv.c"), "w") as fh:
+        fh.write(src)
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), os.path.join(tmp, "srv.c"), "-o",
+                    os.path.join(tmp, "srv")], check=True)
+    got = subprocess.run([os.path.join(tmp, "srv")], capture_output=True, text=True, check=True).stdout.split()
+    assert [int(x) for x in got] == [C.sizeof(rxg.ServerConfig), rxg.ServerConfig.max_bytes.offset,
+                                     rxg.ServerConfig.idle_ms.offset]
 
 
 def test_product_does_not_link_the_oracle():
