@@ -210,7 +210,7 @@ struct rxg_ctx {
         uint32_t rec_kind = 0, blocks = 1, max_frames = 0;
         uint64_t max_bytes = 0, idle_ticks = 0;
         unsigned long long seq = 0;
-        uint64_t seen_writes = ~0ull;  // table_writes as of the last request served
+        uint64_t synced_writes = 0;    // table_writes whose mirror_ev the host has waited for
     } srv;
 };
 
@@ -873,9 +873,12 @@ static int srv_post(rxg_ctx *c, const SrvReq &r)
     rxg_ctx::Server &S = c->srv;
     int rc;
     if ((!S.launched || __atomic_load_n(&S.mbox->exited, __ATOMIC_ACQUIRE)) && (rc = srv_launch(c))) return rc;
+    // the request, then seq2, then seq (x86 stores become visible in order; the server takes
+    // the request when it reads both numbers new, SrvMbox)
     S.mbox->req = r;
     const unsigned long long q = ++S.seq;
-    __atomic_store_n(&S.mbox->seq, q, __ATOMIC_SEQ_CST);  // the request's fields before seq
+    __atomic_store_n(&S.mbox->seq2, q, __ATOMIC_RELEASE);
+    __atomic_store_n(&S.mbox->seq, q, __ATOMIC_SEQ_CST);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spins = 1;; ++spins) {
         if (__atomic_load_n(&S.mbox->done, __ATOMIC_ACQUIRE) == q) break;
@@ -978,7 +981,10 @@ extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b)
     int rc = begin_bursts(c, b->frames, &one, 1, b->rec_kind, "rxg_server_burst_dev");
     if (rc) return rc;
     // mirror writes queued on the context's stream land before the server reads the tables
-    if (c->mirror_ev_set) HIP_OK(hipEventSynchronize(c->mirror_ev));
+    if (c->table_writes != c->srv.synced_writes) {
+        HIP_OK(hipEventSynchronize(c->mirror_ev));
+        c->srv.synced_writes = c->table_writes;
+    }
     if (b->n) {
         SrvReq r;
         std::memset(&r, 0, sizeof r);
@@ -988,11 +994,7 @@ extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b)
         r.out = (uint8_t *)b->out;
         r.n = b->n;
         r.table = table_view(c);
-        // the CUs re-read device memory that changed: mirror tables written since the last
-        // request, or frames outside the server's own (uncached, coherent) staging
-        if (c->table_writes != c->srv.seen_writes || b->frames != c->srv.arena) r.flags |= kSrvInvalidate;
         if ((rc = srv_post(c, r))) return rc;
-        c->srv.seen_writes = c->table_writes;
     }
     c->burst_ok = true;
     return 0;

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include "rxg_common.h"
 
 namespace rxg {
@@ -68,19 +70,26 @@ struct SrvReq {
     const uint16_t *len;
     uint8_t *out;            // records of the server's kind
     uint32_t n;
-    uint32_t flags;          // kSrvInvalidate
+    uint32_t flags;          // reserved (0)
     DevTable table;          // the mirror as of the post
 };
-// SrvReq.flags: device memory the request reads may have changed since the last request
-// (mirror writes, caller-written frames): every workgroup's CU invalidates its L1 first
-constexpr uint32_t kSrvInvalidate = 1u;
-struct SrvMbox {                  // coherent host memory
-    unsigned long long seq;       // host: number of the request posted (release)
-    unsigned long long done;      // server: number of the last request finished (release)
-    unsigned long long stop;      // host: nonzero = exit
-    unsigned long long exited;    // server: nonzero once the kernel has left its loop
+// Coherent host memory.  The first 128 bytes are what the host writes and the server polls,
+// read whole by one wave instruction (16 lanes x 8 bytes): a request is taken when seq and
+// seq2 both show its number (the host writes req, then seq2, then seq; each 64-byte line is
+// read as one snapshot, so both numbers new means every field of both lines is new).  The
+// server's words are on a line of their own.
+struct alignas(128) SrvMbox {
+    unsigned long long seq;       // host: number of the request posted
     SrvReq req;
+    unsigned long long seq2;      // host: = seq, written after req
+    unsigned long long stop;      // host: nonzero = exit
+    unsigned long long hpad[1];
+    alignas(128) unsigned long long done;  // server: number of the last request finished
+    unsigned long long exited;    // server: nonzero once the kernel has left its loop
 };
+static_assert(sizeof(SrvReq) == 88, "mailbox layout");
+static_assert(offsetof(SrvMbox, seq2) == 96 && offsetof(SrvMbox, stop) == 104 && offsetof(SrvMbox, done) == 128,
+              "mailbox layout");
 struct SrvCtl {                   // device memory
     unsigned long long go;        // the request the workgroups run (kSrvStop: exit)
     unsigned int fin;             // workgroups finished, all requests (monotonic)

@@ -2119,27 +2119,46 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
     unsigned long long last = 0ull;  // thread 0: the last request this workgroup saw
     if (threadIdx.x == 0) last = srv_load(&sa.mbox->done, __HIP_MEMORY_SCOPE_SYSTEM);
     for (;;) {
-        if (threadIdx.x == 0) {
+        if (blockIdx.x == 0 && threadIdx.x < 64) {
+            // wave 0 polls the mailbox's first 128 bytes (lane l < 16: bytes 8l .. 8l+7) in
+            // one instruction: the request arrives with its number, no second round trip
+            const int l = (int)threadIdx.x;
+            const unsigned long long lst = __shfl(last, 0, 64);
+            const long long t0 = wall_clock64();
             unsigned long long go;
-            if (blockIdx.x == 0) {
-                const long long t0 = wall_clock64();
-                for (;;) {
-                    if (srv_load(&sa.mbox->stop, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) {
-                        go = kSrvStop;
-                        break;
-                    }
-                    const unsigned long long q = srv_load(&sa.mbox->seq, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (q != last) {
-                        go = q;
-                        break;
-                    }
-                    if ((unsigned long long)(wall_clock64() - t0) > sa.idle_ticks) {
-                        go = kSrvStop;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(4);
+            for (;;) {
+                unsigned long long w = 0ull;
+                if (l < 16)
+                    w = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(sa.mbox) + l, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+                const unsigned long long q = __shfl(w, 0, 64), q2 = __shfl(w, 12, 64), st = __shfl(w, 13, 64);
+                if (st != 0ull) {
+                    go = kSrvStop;
+                    break;
                 }
-                if (go != kSrvStop) s_req = sa.mbox->req;  // ordered after the acquire of seq
+                if (q != lst && q == q2) {
+                    if (l >= 1 && l <= 11) reinterpret_cast<unsigned long long *>(&s_req)[l - 1] = w;  // bytes 8 .. 95
+                    go = q;
+                    break;
+                }
+                if ((unsigned long long)(wall_clock64() - t0) > sa.idle_ticks) {
+                    go = kSrvStop;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            // One acquire per request, not per poll: the CU's L1 may hold lines of the previous
+            // request's staging (host memory, same addresses) or of device memory written since
+            // (mirror tables, caller frames); waited for before any wave of the workgroup loads
+            // (MI355X_MICROARCH.md, inter-workgroup visibility).  A first form with relaxed
+            // polls and no acquire served stale staging lines (test_gpu_server).
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the request's words, written by lanes 1-11, for lane 0
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (l == 0) {
                 // the others hear of a request only when they take part in it (and of stop)
                 if (gridDim.x > 1 && (go == kSrvStop || srv_participants(s_req.n) > 1u)) {
                     if (go != kSrvStop) sa.ctl->req = s_req;
@@ -2148,14 +2167,19 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_store(&sa.ctl->go, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-            } else {
-                for (;;) {
-                    go = srv_load(&sa.ctl->go, __HIP_MEMORY_SCOPE_AGENT);
-                    if (go != last) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (go != kSrvStop) s_req = sa.ctl->req;
+                s_go = go;
+                last = go;
             }
+        } else if (blockIdx.x != 0 && threadIdx.x == 0) {
+            unsigned long long go;
+            for (;;) {  // relaxed polls, then one acquire (MI355X_MICROARCH.md)
+                go = __hip_atomic_load(&sa.ctl->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (go != last) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // this CU's L1 (see workgroup 0)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (go != kSrvStop) s_req = sa.ctl->req;
             s_go = go;
             last = go;
         }
@@ -2166,16 +2190,6 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
         if (blockIdx.x >= P) {  // published for the first P workgroups of a larger grid
             __syncthreads();
             continue;
-        }
-        if (s_req.flags & kSrvInvalidate) {
-            // device-memory inputs (the mirror tables after a write, frames the caller rewrote)
-            // changed since this CU last read them: one agent-scope acquire per CU, waited
-            // for before any wave loads (MI355X_MICROARCH.md, inter-workgroup visibility)
-            if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
         }
         RxArgs a;
         a.frames = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)s_req.frames));
