@@ -174,12 +174,42 @@ def test_server_rejects_bad_requests(srv_engine):
         eng.server_stop()
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_server_replay_sequential_equivalence(srv_engine, seed):
+@pytest.mark.parametrize("seed,on_device", [(1, False), (2, False), (3, True)])
+def test_server_replay_sequential_equivalence(seed, on_device):
     """The replay test of test_gpu_replay (in-burst SYN/FIN writes re-classified) with the
-    burst served instead of launched."""
-    srv_engine.server_start(rxg.REC16, max_frames=4096)
+    burst served instead of launched; on_device: every fix-up a GPU re-classify launch, which
+    reads the served burst's frames in the server's staging."""
+    eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20,
+                     flags=rxg.CFG_REPLAY_ON_DEVICE if on_device else 0)
+    eng.server_start(rxg.REC16, blocks=2, max_frames=4096)
     try:
-        test_gpu_replay.test_replay_sequential_equivalence(srv_engine, seed)
+        test_gpu_replay.test_replay_sequential_equivalence(eng, seed)
     finally:
-        srv_engine.server_stop()
+        eng.close()
+
+
+def test_launched_bursts_beside_a_running_server(srv_engine):
+    """Launched bursts (another stream of the same context) run beside the resident server and
+    interleave with served ones; every record equals the oracle's."""
+    eng = srv_engine
+    rows, frames = pktgen.parity_set(seed=21, n=3000)
+    arena, off, lens = pktgen.pack_arena(frames)
+    tcb, live = pktgen.table_arrays(rows)
+    eng.tcb_load(tcb, live)
+    exp, _ = oracle.rx_batch(arena, off, lens, tcb, live)
+    n = len(lens)
+    d_arena, d_off, d_len = _upload(eng, arena, off, lens)
+    out = eng.alloc(n * 48)
+    eng.server_start(rxg.REC48, blocks=2, max_frames=256)
+    try:
+        for rep in range(3):
+            eng.rx_burst_dev(d_arena.ptr, d_off.ptr, d_len.ptr, n, out.ptr, rxg.REC48)  # launched
+            eng.sync()
+            assert_records_equal(out.download(np.uint8, n * 48).view(rxg.REC48_DTYPE), exp, frames)
+            i = 100 * rep
+            got = eng.rx_burst(frames[i:i + 40], rxg.REC48)  # served
+            assert_records_equal(got, exp[i:i + 40], frames[i:i + 40])
+    finally:
+        eng.server_stop()
+        for d in (d_arena, d_off, d_len, out):
+            d.free()
