@@ -16,6 +16,7 @@
 #include <cstring>
 #include <thread>
 #include <unordered_map>
+#include <immintrin.h>
 #include <vector>
 
 #include "rxg.h"
@@ -196,17 +197,23 @@ struct rxg_ctx {
     uint64_t zc_bytes = 64ull << 20; // host bursts up to this many staged bytes: zero-copy
 
     // latency-mode server (rxg_server_*): a persistent kernel on its own
-    // stream, a mailbox and staging in coherent host memory
+    // stream; the mailbox and the host-burst staging in device memory the host writes through
+    // the BAR (dev = true) or in coherent host memory; answers and records in host memory
     struct Server {
         bool on = false;        // configured (the kernel may have exited idle: relaunched on demand)
         bool launched = false;  // a kernel was launched since the last stream synchronisation
+        bool dev = false;       // arena / off / len in device memory (host writes only)
+        bool mdev = false;      // mbox in device memory (RXG_SRV_DEVICE_MAILBOX)
         hipStream_t st = nullptr;
-        SrvMbox *mbox = nullptr;
+        SrvMbox *mbox = nullptr;  // host-written words: seq, request, stop
+        SrvMbox *ret = nullptr;   // server-written words: done, exited (host memory; = mbox if !mdev)
         SrvCtl *ctl = nullptr;
         uint8_t *arena = nullptr;
         uint32_t *off = nullptr;
         uint16_t *len = nullptr;
         uint8_t *out = nullptr;
+        std::vector<uint32_t> h_off;  // host copies of the packed offsets (device staging is
+        std::vector<uint16_t> h_len;  // write-only from the host: a read would cross PCIe)
         uint32_t rec_kind = 0, blocks = 1, max_frames = 0;
         uint64_t max_bytes = 0, idle_ticks = 0;
         unsigned long long seq = 0;
@@ -846,15 +853,17 @@ static int srv_launch(rxg_ctx *c)
         HIP_OK(hipStreamSynchronize(S.st));
         S.launched = false;
     }
-    __atomic_store_n(&S.mbox->stop, 0ull, __ATOMIC_SEQ_CST);
-    __atomic_store_n(&S.mbox->exited, 0ull, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&S.mbox->stop, 0ull, __ATOMIC_RELEASE);  // plain stores: no locked op over the BAR
+    __atomic_store_n(&S.ret->exited, 0ull, __ATOMIC_SEQ_CST);
+    _mm_sfence();  // device memory is write-combined on the host
     SrvCtl init;
     std::memset(&init, 0, sizeof init);
-    init.go = __atomic_load_n(&S.mbox->done, __ATOMIC_ACQUIRE);  // the workgroups wait past it
+    init.go = __atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE);  // the workgroups wait past it
     HIP_OK(hipMemcpyAsync(S.ctl, &init, sizeof init, hipMemcpyHostToDevice, S.st));
     HIP_OK(hipStreamSynchronize(S.st));
     LaunchServer L;
     L.mbox = S.mbox;
+    L.ret = S.ret;
     L.ctl = S.ctl;
     L.counters = c->counters;
     L.idle_ticks = S.idle_ticks;
@@ -872,24 +881,31 @@ static int srv_post(rxg_ctx *c, const SrvReq &r)
 {
     rxg_ctx::Server &S = c->srv;
     int rc;
-    if ((!S.launched || __atomic_load_n(&S.mbox->exited, __ATOMIC_ACQUIRE)) && (rc = srv_launch(c))) return rc;
-    // the request, then seq2, then seq (x86 stores become visible in order; the server takes
-    // the request when it reads both numbers new, SrvMbox)
+    if ((!S.launched || __atomic_load_n(&S.ret->exited, __ATOMIC_ACQUIRE)) && (rc = srv_launch(c))) return rc;
+    // the staging, the request, then seq2, then seq (the server takes the request when it
+    // reads both numbers new, SrvMbox).  Device memory is write-combined on the host, where
+    // stores may pass each other: each step is fenced (a no-op cost for host memory, whose
+    // x86 stores are already visible in order).
+    _mm_sfence();
     S.mbox->req = r;
+    _mm_sfence();
     const unsigned long long q = ++S.seq;
     __atomic_store_n(&S.mbox->seq2, q, __ATOMIC_RELEASE);
-    __atomic_store_n(&S.mbox->seq, q, __ATOMIC_SEQ_CST);
+    _mm_sfence();
+    __atomic_store_n(&S.mbox->seq, q, __ATOMIC_RELEASE);
+    _mm_sfence();
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spins = 1;; ++spins) {
-        if (__atomic_load_n(&S.mbox->done, __ATOMIC_ACQUIRE) == q) break;
+        if (__atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE) == q) break;
         __builtin_ia32_pause();
         if ((spins & 1023u) == 0u) {
-            if (__atomic_load_n(&S.mbox->exited, __ATOMIC_ACQUIRE)) {
-                if (__atomic_load_n(&S.mbox->done, __ATOMIC_ACQUIRE) == q) break;
+            if (__atomic_load_n(&S.ret->exited, __ATOMIC_ACQUIRE)) {
+                if (__atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE) == q) break;
                 if ((rc = srv_launch(c))) return rc;
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
-                __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_SEQ_CST);
+                __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_RELEASE);
+                _mm_sfence();
                 return fail(-ETIMEDOUT, "rxg_server: request %llu not served in 10 s", q);
             }
         }
@@ -900,8 +916,11 @@ static int srv_post(rxg_ctx *c, const SrvReq &r)
 static void srv_free(rxg_ctx *c)
 {
     rxg_ctx::Server &S = c->srv;
-    for (void *h : {(void *)S.mbox, (void *)S.arena, (void *)S.off, (void *)S.len, (void *)S.out})
-        if (h) (void)hipHostFree(h);
+    if (S.mbox) (void)(S.mdev ? hipFree(S.mbox) : hipHostFree(S.mbox));
+    for (void *h : {(void *)S.arena, (void *)S.off, (void *)S.len})
+        if (h) (void)(S.dev ? hipFree(h) : hipHostFree(h));
+    if (S.ret && S.ret != S.mbox) (void)hipHostFree(S.ret);
+    if (S.out) (void)hipHostFree(S.out);
     if (S.ctl) (void)hipFree(S.ctl);
     if (S.st) (void)hipStreamDestroy(S.st);
     S = rxg_ctx::Server{};
@@ -916,7 +935,8 @@ extern "C" int rxg_server_stop(rxg_ctx *c)
     rxg_ctx::Server &S = c->srv;
     hipError_t e = hipSuccess;
     if (S.launched) {
-        __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_SEQ_CST);
+        __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_RELEASE);
+        _mm_sfence();
         e = hipStreamSynchronize(S.st);
     }
     srv_free(c);
@@ -944,19 +964,40 @@ extern "C" int rxg_server_start(rxg_ctx *c, const rxg_server_config *cfg)
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0)
         khz = 100000;  // 100 MHz, the MI300-series constant clock
     S.idle_ticks = (uint64_t)(cfg->idle_ms ? cfg->idle_ms : 1000u) * (uint64_t)khz;
+    // Placement: with a large BAR the host writes the staged frames and
+    // descriptors into fine-grained device memory (posted PCIe writes) and the server reads
+    // them from HBM; otherwise they are coherent host memory the server reads over PCIe.  The
+    // mailbox stays in host memory unless RXG_SRV_DEVICE_MAILBOX.
+    int large_bar = 0;
+    if (!(cfg->flags & RXG_SRV_HOST_STAGING) &&
+        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) != hipSuccess)
+        large_bar = 0;
+    S.dev = large_bar != 0;
+    S.mdev = S.dev && (cfg->flags & RXG_SRV_DEVICE_MAILBOX);
     const unsigned flags = hipHostMallocCoherent | hipHostMallocMapped;
+    auto place = [&](bool dev, void **p, size_t bytes) {
+        return dev ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained) == hipSuccess
+                   : hipHostMalloc(p, bytes, flags) == hipSuccess;
+    };
     bool ok = hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) == hipSuccess &&
-              hipHostMalloc((void **)&S.mbox, sizeof(SrvMbox), flags) == hipSuccess &&
-              hipHostMalloc((void **)&S.arena, S.max_bytes, flags) == hipSuccess &&
-              hipHostMalloc((void **)&S.off, (size_t)maxf * 4u, flags) == hipSuccess &&
-              hipHostMalloc((void **)&S.len, (size_t)maxf * 2u, flags) == hipSuccess &&
+              place(S.mdev, (void **)&S.mbox, sizeof(SrvMbox)) && place(S.dev, (void **)&S.arena, S.max_bytes) &&
+              place(S.dev, (void **)&S.off, (size_t)maxf * 4u) && place(S.dev, (void **)&S.len, (size_t)maxf * 2u) &&
               hipHostMalloc((void **)&S.out, (size_t)maxf * cfg->rec_kind, flags) == hipSuccess &&
               hipMalloc((void **)&S.ctl, sizeof(SrvCtl)) == hipSuccess;
+    if (ok && S.mdev) ok = hipHostMalloc((void **)&S.ret, sizeof(SrvMbox), flags) == hipSuccess;
     if (!ok) {
         srv_free(c);
         return fail(-ENOMEM, "rxg_server_start: mailbox / staging for %u frames", maxf);
     }
-    std::memset(S.mbox, 0, sizeof(SrvMbox));
+    if (!S.mdev) S.ret = S.mbox;
+    S.h_off.assign(maxf, 0u);
+    S.h_len.assign(maxf, 0u);
+    if (S.mdev) {
+        HIP_OK(hipMemset(S.mbox, 0, sizeof(SrvMbox)));
+        std::memset(S.ret, 0, sizeof(SrvMbox));
+    } else {
+        std::memset(S.mbox, 0, sizeof(SrvMbox));
+    }
     S.on = true;
     if ((rc = srv_launch(c))) {
         srv_free(c);
@@ -966,6 +1007,12 @@ extern "C" int rxg_server_start(rxg_ctx *c, const rxg_server_config *cfg)
 }
 
 extern "C" int rxg_server_active(rxg_ctx *c) { return c && c->srv.on ? 1 : 0; }
+
+extern "C" int rxg_server_placement(rxg_ctx *c)
+{
+    if (!c || !c->srv.on) return RXG_SRV_NONE;
+    return c->srv.dev ? RXG_SRV_DEVICE : RXG_SRV_HOST;
+}
 
 extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b)
 {
@@ -1043,15 +1090,19 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
         for (uint32_t i = 0; i < n && fits; ++i) {
             const uint64_t need = (pkts[i].data_len + 63u) / 64u;
             fits = (slot + need) * 64u <= S.max_bytes;
-            S.off[i] = (uint32_t)slot;
-            S.len[i] = pkts[i].data_len;
+            S.h_off[i] = (uint32_t)slot;
+            S.h_len[i] = pkts[i].data_len;
             slot += need;
         }
         if (fits) {
+            // write-only streams into the staging (device memory: write-combined, never read
+            // back by the host); srv_post fences them before the request
             for (uint32_t i = 0; i < n; ++i)
                 if (pkts[i].data_len)
-                    std::memcpy(S.arena + (uint64_t)S.off[i] * 64u,
+                    std::memcpy(S.arena + (uint64_t)S.h_off[i] * 64u,
                                 (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off, pkts[i].data_len);
+            std::memcpy(S.off, S.h_off.data(), (size_t)n * 4u);
+            std::memcpy(S.len, S.h_len.data(), (size_t)n * 2u);
             rxg_dev_batch b;
             b.frames = S.arena;
             b.off64 = S.off;

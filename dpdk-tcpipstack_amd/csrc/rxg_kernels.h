@@ -98,7 +98,8 @@ struct SrvCtl {                   // device memory
 };
 constexpr unsigned long long kSrvStop = ~0ull;
 struct LaunchServer {
-    SrvMbox *mbox;
+    SrvMbox *mbox;                  // host-written words (host or device memory)
+    SrvMbox *ret;                   // done / exited (host memory); nullptr = mbox
     SrvCtl *ctl;
     unsigned long long *counters;
     unsigned long long idle_ticks;  // wall-clock ticks without a request before the kernel exits

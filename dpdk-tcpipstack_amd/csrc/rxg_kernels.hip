@@ -2085,7 +2085,8 @@ __global__ __launch_bounds__(256, WPE ? WPE : ((STRIP & 32768) ? 3 : 1)) void rx
 // clock (the host relaunches on its next burst), so a server whose process is gone ends by
 // itself.  STRIP (experiment builds): the rx body's form (32768 = pipelined rounds).
 struct SrvArgs {
-    SrvMbox *mbox;
+    SrvMbox *mbox;  // the host-written words (seq, request, stop): host memory or device memory
+    SrvMbox *ret;   // the server's words (done, exited): host memory (= mbox when it is there)
     SrvCtl *ctl;
     unsigned long long *counters;
     unsigned long long idle_ticks;
@@ -2117,7 +2118,7 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
     __shared__ SrvReq s_req;
     __shared__ unsigned long long s_go;
     unsigned long long last = 0ull;  // thread 0: the last request this workgroup saw
-    if (threadIdx.x == 0) last = srv_load(&sa.mbox->done, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) last = srv_load(&sa.ret->done, __HIP_MEMORY_SCOPE_SYSTEM);
     for (;;) {
         if (blockIdx.x == 0 && threadIdx.x < 64) {
             // wave 0 polls the mailbox's first 128 bytes (lane l < 16: bytes 8l .. 8l+7) in
@@ -2211,26 +2212,29 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
         a.b[0].slice0 = 0u;
         a.nslices = (a.b[0].n + 63u) / 64u;
         rx_body<MODE, 0xFF, true, STRIP, false, 11, false, false, true, false, 0>(a, blockIdx.x, P);
-        // this wave's records have reached their memory before `done`
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        // Every wave's stores have reached the L2 (vmcnt), then ONE system-scope release per
+        // workgroup writes this XCD's L2 back (buffer_wbl2 covers the whole cache, so one
+        // per workgroup covers its four waves; it used to run once per wave and once more
+        // before `done`), before the workgroup counts itself finished
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bool lastp = true;
             if (P > 1u) {
                 lastp = atomicAdd(&sa.ctl->fin, 1u) + 1u == P;
-                if (lastp) atomicExch(&sa.ctl->fin, 0u);  // before `done`: the next request counts from 0
+                if (lastp) {
+                    atomicExch(&sa.ctl->fin, 0u);  // before `done`: the next request counts from 0
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
-            if (lastp) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(&sa.mbox->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            if (lastp) __hip_atomic_store(&sa.ret->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();  // s_req and s_go are rewritten by the next request
     }
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(&sa.mbox->exited, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&sa.ret->exited, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------ synthetic frames ---
@@ -2607,7 +2611,7 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
 
 hipError_t launch_server(const LaunchServer &L, hipStream_t st)
 {
-    SrvArgs sa{L.mbox, L.ctl, L.counters, L.idle_ticks};
+    SrvArgs sa{L.mbox, L.ret ? L.ret : L.mbox, L.ctl, L.counters, L.idle_ticks};
     const dim3 g(L.blocks ? L.blocks : 1u), b(256);
     // the streaming classes' rounds software-pipelined (STRIP 32768): a served burst's frame
     // reads are latency-bound (one wave per 64 frames, often over PCIe), and the second

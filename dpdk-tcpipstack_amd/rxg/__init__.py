@@ -32,6 +32,10 @@ STATE_NONE = 0xFF
 V_DISPATCH, V_RST_NOPCB, V_RST_LISTEN_NONSYN, V_DROP_NONTCP, V_ARP, V_DROP_L2 = range(6)
 F_IP_OK, F_TCP_OK, F_LISTEN, F_REF_NULLSLOT, F_TRUNC, F_ARP_LEARN = 1, 2, 4, 8, 16, 32
 REC8, REC16, REC48 = 8, 16, 48
+# rxg_server_config.flags and rxg_server_placement (include/rxg.h)
+SRV_HOST_STAGING = 1
+SRV_DEVICE_MAILBOX = 2
+SRV_NONE, SRV_HOST, SRV_DEVICE = 0, 1, 2
 
 COUNTERS = ["rx", "bytes", "ipv4", "arp", "other_l2", "tcp", "non_tcp", "ip_cksum_bad",
             "tcp_cksum_bad", "tcb_hit_exact", "tcb_hit_listen", "nopcb", "listen_nonsyn",
@@ -129,7 +133,7 @@ class DevBatch(C.Structure):
 class ServerConfig(C.Structure):
     """rxg_server_config: latency mode (rxg_server_start)."""
     _fields_ = [("rec_kind", C.c_uint32), ("blocks", C.c_uint32), ("max_frames", C.c_uint32),
-                ("max_bytes", C.c_uint32), ("idle_ms", C.c_uint32), ("pad", C.c_uint32)]
+                ("max_bytes", C.c_uint32), ("idle_ms", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class DevBurst(C.Structure):
@@ -236,6 +240,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
         "rxg_tx_cksum_dev": (C.c_int, [vp, C.POINTER(DevTxBatch), vp]),
         "rxg_server_start": (C.c_int, [vp, C.POINTER(ServerConfig)]),
+        "rxg_server_placement": (C.c_int, [vp]),
         "rxg_server_stop": (C.c_int, [vp]),
         "rxg_server_active": (C.c_int, [vp]),
         "rxg_server_burst_dev": (C.c_int, [vp, C.POINTER(DevBatch)]),
@@ -572,9 +577,13 @@ class Engine:
 
     # --- latency mode (rxg_server_*): a persistent kernel serves small bursts
     def server_start(self, rec_kind: int = REC8, blocks: int = 1, max_frames: int = 4096,
-                     max_bytes: int = 0, idle_ms: int = 1000):
-        cfg = ServerConfig(rec_kind, blocks, max_frames, max_bytes, idle_ms, 0)
+                     max_bytes: int = 0, idle_ms: int = 1000, flags: int = 0):
+        cfg = ServerConfig(rec_kind, blocks, max_frames, max_bytes, idle_ms, flags)
         _check(_lib.rxg_server_start(self.ctx, C.byref(cfg)), "rxg_server_start")
+
+    def server_placement(self) -> int:
+        """SRV_NONE / SRV_HOST (coherent host memory) / SRV_DEVICE (device memory, BAR writes)."""
+        return int(_lib.rxg_server_placement(self.ctx))
 
     def server_stop(self):
         _check(_lib.rxg_server_stop(self.ctx), "rxg_server_stop")

@@ -372,10 +372,16 @@ int rxg_rx_burst(rxg_ctx *ctx, const rxg_pkt_view *pkts, uint32_t n, uint32_t re
 /* Latency mode for the reference's own burst size (MAX_PKT_BURST = 32, main.c:116; the loop
    main.c:391-399 runs once per rte_eth_rx_burst).  A launched burst pays a kernel launch
    and a stream synchronisation (~20 us for 32 frames); the server is a persistent set of
-   `blocks` workgroups of the same kernel body that polls a mailbox in coherent host memory,
-   so a burst costs the PCIe round trips of its frames and records.  While the server runs,
+   `blocks` workgroups of the same kernel body that polls a mailbox, so a burst costs the
+   PCIe trips of its frames and records.  The host-burst staging (frames, descriptors)
+   lives in device memory the host writes through the PCIe BAR (posted writes; the server
+   reads HBM) when the device exposes its memory to the host (large BAR), else in coherent
+   host memory (RXG_SRV_HOST_STAGING forces that); the mailbox is coherent host memory the
+   server polls (RXG_SRV_DEVICE_MAILBOX moves it to device memory too, measured slower);
+   the server's answers and the records of host bursts are written to host memory.
+   While the server runs,
    rxg_rx_burst sends bursts of up to max_frames frames (max_bytes staged bytes) and of
-   record kind rec_kind through it (packed into the server's own coherent staging), and
+   record kind rec_kind through it (packed into the server's own staging), and
    rxg_server_burst_dev serves device-visible batches.  Records, counters, replay and
    payload gather are those of the launched path.  The server exits by itself after idle_ms
    without a burst (and is relaunched by the next one), so it never outlives its process for
@@ -386,13 +392,21 @@ typedef struct rxg_server_config {
     uint32_t max_frames;  /* largest burst served; 0 = 4096 */
     uint32_t max_bytes;   /* staging bytes for host bursts; 0 = max_frames * 2048 */
     uint32_t idle_ms;     /* exit after this long without a burst; 0 = 1000 */
-    uint32_t pad;
+    uint32_t flags;       /* RXG_SRV_*; 0 = mailbox and staging placed by the device */
 } rxg_server_config;
+#define RXG_SRV_HOST_STAGING 1u   /* staging in coherent host memory */
+#define RXG_SRV_DEVICE_MAILBOX 2u /* mailbox in device memory (large BAR only) */
 int rxg_server_start(rxg_ctx *ctx, const rxg_server_config *cfg);
 /* Stops the server and waits for its kernel to end; 0 if none runs. */
 int rxg_server_stop(rxg_ctx *ctx);
 /* 1 if a server is configured (running or idle-exited, relaunched on demand), else 0. */
 int rxg_server_active(rxg_ctx *ctx);
+/* Where the configured server's host-burst staging lives: RXG_SRV_DEVICE (device memory
+   written through the BAR), RXG_SRV_HOST (coherent host memory), RXG_SRV_NONE (no server). */
+#define RXG_SRV_NONE 0
+#define RXG_SRV_HOST 1
+#define RXG_SRV_DEVICE 2
+int rxg_server_placement(rxg_ctx *ctx);
 /* Classify a device-visible batch (HBM or mapped host memory) through the server:
    b->rec_kind must be the server's, b->n <= max_frames.  Synchronous: returns once the
    records are written at b->out.  -ENODEV without a server. */

@@ -7,6 +7,11 @@
   dev-1      rxg_server_burst_dev of ONE device-resident frame: the mailbox round trip floor
   dev-n      rxg_server_burst_dev of the burst's frames resident in HBM (no PCIe frame reads)
 
+The served columns are measured for both placements of the mailbox and staging, one after
+the other in the same process: "device" staging (device memory the host writes through the
+BAR, the default on a large-BAR GPU), "_hostmem" (RXG_SRV_HOST_STAGING, coherent host memory)
+and "_devmbox" (RXG_SRV_DEVICE_MAILBOX: the mailbox in device memory too).
+
 python scripts/srvlat.py [--blocks 4]   (one JSON line per frame size and burst)"""
 import argparse
 import ctypes as C
@@ -70,10 +75,12 @@ def main():
                 eng.server_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, d_out.ptr, rxg.REC8)
             row = {"frame_bytes": size, "n": n, "launched": per_call_us(burst_replay),
                    "launched_nr": per_call_us(burst)}
-            eng.server_start(rxg.REC8, blocks=args.blocks, max_frames=nmax)
-            row.update({"served": per_call_us(burst_replay), "served_nr": per_call_us(burst),
-                        "dev": per_call_us(dev)})
-            eng.server_stop()
+            for tag, flags in (("", 0), ("_hostmem", rxg.SRV_HOST_STAGING), ("_devmbox", rxg.SRV_DEVICE_MAILBOX)):
+                eng.server_start(rxg.REC8, blocks=args.blocks, max_frames=nmax, flags=flags)
+                row["placement" + tag] = {rxg.SRV_DEVICE: "device", rxg.SRV_HOST: "host"}[eng.server_placement()]
+                row.update({"served" + tag: per_call_us(burst_replay), "served_nr" + tag: per_call_us(burst),
+                            "dev" + tag: per_call_us(dev)})
+                eng.server_stop()
             print(json.dumps(row), flush=True)
         d_out.free()
         for v in b.values():

@@ -120,6 +120,7 @@ def test_group_and_null_arguments_fail_loudly():
     assert lib.rxg_server_start(None, C.byref(cfg)) == -22
     assert lib.rxg_server_stop(None) == -22
     assert lib.rxg_server_active(None) == 0
+    assert lib.rxg_server_placement(None) == 0
     assert lib.rxg_server_burst_dev(None, None) == -22
 
 

@@ -1,7 +1,8 @@
 """GPU: latency mode (include/rxg.h rxg_server_*).  A persistent kernel serves bursts posted
-through a host-coherent mailbox; its records, counters and replay must equal the launched
-path's and the oracle's, burst after burst (fresh frame content each time: no stale reads of
-host memory), across mirror writes, idle exits and restarts."""
+through a mailbox (device memory the host writes through the BAR, or coherent host memory:
+both placements are tested); its records, counters and replay must equal the launched path's
+and the oracle's, burst after burst (fresh frame content each time: no stale reads of the
+staging), across mirror writes, idle exits and restarts."""
 import time
 
 import numpy as np
@@ -23,12 +24,31 @@ def srv_engine():
     eng.close()
 
 
+# rxg_server_config.flags: 0 = placed by the device (device memory on a large-BAR GPU),
+# SRV_HOST_STAGING = coherent host memory
+PLACEMENTS = [0, rxg.SRV_HOST_STAGING, rxg.SRV_DEVICE_MAILBOX]
+
+
+def test_server_placement_reported(srv_engine):
+    """flags 0 puts the mailbox and staging in device memory when the GPU exposes it to the
+    host (large BAR, as on the MI355X boxes); RXG_SRV_HOST_STAGING keeps them in host memory."""
+    eng = srv_engine
+    assert eng.server_placement() == rxg.SRV_NONE
+    eng.server_start(rxg.REC8, max_frames=64, flags=rxg.SRV_HOST_STAGING)
+    assert eng.server_placement() == rxg.SRV_HOST
+    eng.server_start(rxg.REC8, max_frames=64)
+    assert eng.server_placement() in (rxg.SRV_DEVICE, rxg.SRV_HOST)
+    eng.server_stop()
+    assert eng.server_placement() == rxg.SRV_NONE
+
+
 def _upload(eng, arena, off, lens):
     return eng.to_device(arena), eng.to_device(off.astype(np.uint32)), eng.to_device(lens.astype(np.uint16))
 
 
+@pytest.mark.parametrize("flags", PLACEMENTS)
 @pytest.mark.parametrize("blocks", [1, 3])
-def test_server_bursts_equal_launched(srv_engine, blocks):
+def test_server_bursts_equal_launched(srv_engine, blocks, flags):
     """Sub-bursts of every shape (1 .. 4096 frames, partial slices) of one device batch: the
     served records equal one launched burst's, byte for byte, and so do the counters."""
     eng = srv_engine
@@ -46,7 +66,7 @@ def test_server_bursts_equal_launched(srv_engine, blocks):
         eng.sync()
         exp_cnt = eng.counters()
         exp = ref.download(np.uint8, n * 16)
-        eng.server_start(rxg.REC16, blocks=blocks, max_frames=4096)
+        eng.server_start(rxg.REC16, blocks=blocks, max_frames=4096, flags=flags)
         assert eng.server_active()
         eng.counters_reset()
         i = 0
@@ -67,8 +87,9 @@ def test_server_bursts_equal_launched(srv_engine, blocks):
             d.free()
 
 
+@pytest.mark.parametrize("flags", PLACEMENTS)
 @pytest.mark.parametrize("rec", [rxg.REC8, rxg.REC16, rxg.REC48])
-def test_server_host_bursts_equal_launched_and_oracle(srv_engine, rec):
+def test_server_host_bursts_equal_launched_and_oracle(srv_engine, rec, flags):
     """rxg_rx_burst through the server: 200 consecutive bursts of the reference's size class
     (1..64 frames, fresh content every burst) equal the same bursts launched, and (REC48,
     every field) the oracle."""
@@ -82,7 +103,7 @@ def test_server_host_bursts_equal_launched_and_oracle(srv_engine, rec):
         k = int(rng.integers(1, 65))
         bursts.append(frames[i:i + k])
         i += k
-    eng.server_start(rec, max_frames=256)
+    eng.server_start(rec, max_frames=256, flags=flags)
     try:
         served = [eng.rx_burst(b, rec) for b in bursts]
     finally:
@@ -95,8 +116,9 @@ def test_server_host_bursts_equal_launched_and_oracle(srv_engine, rec):
             assert_records_equal(got, exp, b)
 
 
+@pytest.mark.parametrize("flags", PLACEMENTS)
 @pytest.mark.parametrize("blocks", [1, 3])
-def test_server_sees_mirror_writes(srv_engine, blocks):
+def test_server_sees_mirror_writes(srv_engine, blocks, flags):
     """tcbs[] writes between served bursts (upsert, remove, set_state) are on the device
     before the next burst reads the table: each served burst equals the oracle on the table
     as it stands."""
@@ -104,7 +126,7 @@ def test_server_sees_mirror_writes(srv_engine, blocks):
     rows, frames = pktgen.parity_set(seed=5, n=1024, nflows=64)
     tcb, live = pktgen.table_arrays(rows)
     eng.tcb_load(tcb, live)
-    eng.server_start(rxg.REC48, blocks=blocks, max_frames=512)
+    eng.server_start(rxg.REC48, blocks=blocks, max_frames=512, flags=flags)
     rng = np.random.default_rng(5 + blocks)
     try:
         for step in range(30):
@@ -130,7 +152,8 @@ def test_server_sees_mirror_writes(srv_engine, blocks):
         eng.server_stop()
 
 
-def test_server_idle_exit_and_relaunch(srv_engine):
+@pytest.mark.parametrize("flags", PLACEMENTS)
+def test_server_idle_exit_and_relaunch(srv_engine, flags):
     """A server idle for longer than idle_ms exits; the next burst relaunches it.  Stop and
     start again; a context closed with a running server stops it."""
     eng = srv_engine
@@ -139,7 +162,7 @@ def test_server_idle_exit_and_relaunch(srv_engine):
     eng.tcb_load(tcb, live)
     arena, off, lens = pktgen.pack_arena(frames[:40])
     exp = eng.rx_arena(arena, off, lens, rxg.REC16)
-    eng.server_start(rxg.REC16, max_frames=64, idle_ms=30)
+    eng.server_start(rxg.REC16, max_frames=64, idle_ms=30, flags=flags)
     for _ in range(3):
         assert eng.rx_burst(frames[:40], rxg.REC16).tobytes() == exp.tobytes()
         time.sleep(0.15)  # the kernel exits idle
@@ -174,14 +197,15 @@ def test_server_rejects_bad_requests(srv_engine):
         eng.server_stop()
 
 
-@pytest.mark.parametrize("seed,on_device", [(1, False), (2, False), (3, True)])
-def test_server_replay_sequential_equivalence(seed, on_device):
+@pytest.mark.parametrize("seed,on_device,flags", [(1, False, 0), (2, False, rxg.SRV_HOST_STAGING), (3, True, 0),
+                                                  (4, True, rxg.SRV_HOST_STAGING)])
+def test_server_replay_sequential_equivalence(seed, on_device, flags):
     """The replay test of test_gpu_replay (in-burst SYN/FIN writes re-classified) with the
     burst served instead of launched; on_device: every fix-up a GPU re-classify launch, which
     reads the served burst's frames in the server's staging."""
     eng = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20,
                      flags=rxg.CFG_REPLAY_ON_DEVICE if on_device else 0)
-    eng.server_start(rxg.REC16, blocks=2, max_frames=4096)
+    eng.server_start(rxg.REC16, blocks=2, max_frames=4096, flags=flags)
     try:
         test_gpu_replay.test_replay_sequential_equivalence(eng, seed)
     finally:
