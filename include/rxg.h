@@ -250,7 +250,10 @@ int rxg_tcb_load(rxg_ctx *ctx, const rxg_tcb_tuple *tcbs, const uint8_t *live, i
    changes O(1) device words (a bucket slot, a listener entry), applied by one small kernel
    on the context's stream after every launch that still reads the old table, whatever its
    stream; a burst on another stream waits for them on the device, not on the host.  Only
-   rxg_tcb_load and growth past load 1/2 rebuild (and upload) the whole table. */
+   rxg_tcb_load and growth past load 1/2 rebuild (and upload) the whole table.  The order
+   against a burst on a caller stream is taken when the write is pushed (an event recorded
+   on that stream then), not per launch: such a stream stays valid until the context's next
+   table write or rxg_fini, or is synchronised before it is destroyed. */
 int rxg_tcb_sync(rxg_ctx *ctx);
 /* Current Ntcb of the mirror. */
 int32_t rxg_tcb_count(rxg_ctx *ctx);

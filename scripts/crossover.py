@@ -35,6 +35,8 @@ import oracle  # noqa: E402
 import rxg  # noqa: E402
 
 BURSTS = [32, 256, 4096, 65536]
+# the served bursts, finer around the one-peer crossover
+SRV_BURSTS = [32, 64, 96, 128, 160, 192, 256, 4096]
 SIZES = [64, 1500]
 FLOWS = [1, 1000, 65536]
 
@@ -94,7 +96,8 @@ def main():
             srv = {}
             for blocks in (1, 4):
                 eng.server_start(rxg.REC8, blocks=blocks, max_frames=4096)
-                srv[blocks] = {n: round(rxg_burst_us(eng, lib, views, ptrs, out, n), 1) for n in BURSTS if n <= 4096}
+                srv_dev = eng.server_placement() == rxg.SRV_DEVICE
+                srv[blocks] = {n: round(rxg_burst_us(eng, lib, views, ptrs, out, n), 1) for n in SRV_BURSTS}
                 eng.server_stop()
             sample = 4096 if flows < 65536 else 1024
             cpu = {}
@@ -110,8 +113,9 @@ def main():
                    "cpu_mpps": {k: round(1.0 / v, 4) for k, v in cpu.items()},
                    # smallest measured burst at which rxg's burst time is below the CPU's n x per-packet
                    "crossover_burst": {k: next((n for n in BURSTS if g[n] < n * v), None) for k, v in cpu.items()},
-                   "crossover_burst_server": {k: next((n for n in BURSTS if min(g[n], *(s.get(n, 1e9) for s in srv.values())) < n * v), None)
+                   "crossover_burst_server": {k: next((n for n in SRV_BURSTS if min(s[n] for s in srv.values()) < n * v), None)
                                               for k, v in cpu.items()},
+                   "server_placement": "device staging (large BAR)" if srv_dev else "host staging",
                    "cpu_sample": f"first {sample} frames, ARP list learned from them, 1 core"}
             rows.append(row)
             print(json.dumps(row), flush=True)

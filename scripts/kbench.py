@@ -42,11 +42,15 @@ def main():
     ap.add_argument("--seed", type=int, default=77, help="copy c is synthesised with seed + c * seed_step")
     ap.add_argument("--seed-step", type=int, default=1, help="17 with bench.py's seed reproduces its batches")
     ap.add_argument("--tx", action="store_true", help="time rxg_tx_cksum_dev (rx_kernel<0>) instead")
+    ap.add_argument("--stream", action="store_true",
+                    help="launch and time on a caller stream (a torch stream), not the context's own: "
+                         "the table-reader ordering of DESIGN.md §2.4 runs per launch")
     ap.add_argument("--check", action="store_true",
                     help="also compare every variant's records (and counters) with the first variant's")
     args = ap.parse_args()
 
     base = rxg.Engine(0)
+    st = torch.cuda.Stream(device=0).cuda_stream if args.stream else None
     wls = {}
     for w in args.workloads.split(","):
         L, flows, mix, copies = WL[w]
@@ -105,15 +109,17 @@ def main():
                     elif args.tx:  # the batch's checksums are already right: rewriting keeps them
                         eng.tx_cksum_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, nfr)
                     else:
-                        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, nfr, out.ptr, args.rec)
+                        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, nfr, out.ptr, args.rec, st)
                 for i in range(2):
                     launch(bs[i % len(bs)])
                 for i in range(args.iters):
                     b = bs[(i + 2) % len(bs)]
-                    eng.record(evs[i][0])
+                    eng.record(evs[i][0], st)
                     launch(b)
-                    eng.record(evs[i][1])
+                    eng.record(evs[i][1], st)
                 eng.sync()
+                if st is not None:
+                    torch.cuda.synchronize(0)
                 ms = [eng.elapsed_ms(a, b) for a, b in evs]
                 res[(v, w)].append(ms)
                 for a, b in evs:
