@@ -159,6 +159,9 @@ def time_workload(eng, wl, steps, warmup, device, stream):
     barrier(device)
     elapsed = time.perf_counter() - t0
     kern_ms = [eng.elapsed_ms(a, b) for a, b in evs]
+    for a, b in evs:
+        eng.event_destroy(a)
+        eng.event_destroy(b)
     return elapsed, kern_ms
 
 

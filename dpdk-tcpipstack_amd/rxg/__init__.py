@@ -715,6 +715,9 @@ class Engine:
         _check(_lib.rxg_event_create(self.ctx, C.byref(e)), "rxg_event_create")
         return e.value
 
+    def event_destroy(self, ev):
+        _check(_lib.rxg_event_destroy(self.ctx, ev), "rxg_event_destroy")
+
     def record(self, ev, stream=None):
         _check(_lib.rxg_event_record(self.ctx, ev, stream), "rxg_event_record")
 
