@@ -95,7 +95,7 @@ struct rxg_ctx {
     // recorded on each such stream and `stream` waits for it (one entry per stream, so a
     // reader on s1 followed by one on s2 are both waited for).  Recording at the write, not
     // after every launch, keeps the caller's stream free of per-launch marker packets (C4 on
-    // a caller stream 78.6 -> 73.5 us per launch, C2 23.9 -> 19.2).
+    // a caller stream 77.9 -> 73.4 us per launch, C2 23.7 -> 19.9).
     hipEvent_t mirror_ev = nullptr;
     bool mirror_ev_set = false;
     uint64_t table_writes = 0;  // mirror_ev recordings (device table writes) so far
@@ -200,8 +200,9 @@ struct rxg_ctx {
     uint64_t zc_bytes = 64ull << 20; // host bursts up to this many staged bytes: zero-copy
 
     // latency-mode server (rxg_server_*): a persistent kernel on its own
-    // stream; the mailbox and the host-burst staging in device memory the host writes through
-    // the BAR (dev = true) or in coherent host memory; answers and records in host memory
+    // stream; the host-burst staging in device memory the host writes through the BAR
+    // (dev = true) or in coherent host memory; the mailbox, answers and records in host
+    // memory (the mailbox in device memory only with RXG_SRV_DEVICE_MAILBOX)
     struct Server {
         bool on = false;        // configured (the kernel may have exited idle: relaunched on demand)
         bool launched = false;  // a kernel was launched since the last stream synchronisation
