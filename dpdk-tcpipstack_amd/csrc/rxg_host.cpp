@@ -91,11 +91,11 @@ struct rxg_ctx {
     // Ordering of table writes against the kernels that read the tables:
     // mirror writes run on `stream`; a burst on another stream waits for mirror_ev (once per
     // write), and the next mirror write waits for every stream other than `stream` that
-    // launched a table-reading kernel since the last write: at the write, an event is
-    // recorded on each such stream and `stream` waits for it (one entry per stream, so a
-    // reader on s1 followed by one on s2 are both waited for).  Recording at the write, not
-    // after every launch, keeps the caller's stream free of per-launch marker packets (C4 on
-    // a caller stream 77.9 -> 73.4 us per launch, C2 23.7 -> 19.9).
+    // launched a table-reading kernel since the last write (one entry per stream, so a
+    // reader on s1 followed by one on s2 are both waited for): the event recorded after the
+    // stream's latest such launch, or, with RXG_CFG_STREAMS_OUTLIVE_WRITES, recorded on the
+    // stream at the write, which keeps the caller's stream free of a marker packet per launch
+    // (C4 on a caller stream 78.2 -> 73.2 us per launch, C2 24.5 -> 20.3).
     hipEvent_t mirror_ev = nullptr;
     bool mirror_ev_set = false;
     uint64_t table_writes = 0;  // mirror_ev recordings (device table writes) so far
@@ -103,6 +103,7 @@ struct rxg_ctx {
         hipStream_t s;
         hipEvent_t e;
         bool pending;     // `s` launched a table reader since the last write (not yet waited for)
+        bool recorded;    // e was recorded after that launch (per-launch mode)
         uint64_t waited;  // table_writes when `s` last waited for mirror_ev (~0: never)
     };
     std::vector<Reader> readers;
@@ -128,6 +129,7 @@ struct rxg_ctx {
     bool touched_all = false;            // whole table replaced
     bool touched_pass2 = false;          // min_null moved (the pass-2 NULL-slot flag)
     bool replay_on_device = false;       // RXG_CFG_REPLAY_ON_DEVICE
+    bool lazy_readers = false;           // RXG_CFG_STREAMS_OUTLIVE_WRITES
     uint64_t rp_stats[4] = {0, 0, 0, 0}; // marked, host fix-ups, device fix-ups, launches
 
     // the last burst's device batch (re-classification reads it again)
@@ -283,6 +285,7 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     }
     if (cfg) {
         c->replay_on_device = (cfg->flags & RXG_CFG_REPLAY_ON_DEVICE) != 0;
+        c->lazy_readers = (cfg->flags & RXG_CFG_STREAMS_OUTLIVE_WRITES) != 0;
         c->max_blocks = cfg->max_blocks;
         if (cfg->zc_bytes) c->zc_bytes = cfg->zc_bytes;
     }
@@ -347,7 +350,7 @@ extern "C" int rxg_fini(rxg_ctx *c)
     (void)rxg_server_stop(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &r : c->readers)  // table readers still running on caller streams
-        if (r.pending && hipEventRecord(r.e, r.s) == hipSuccess)  // (a destroyed stream has finished)
+        if (r.pending && (r.recorded || hipEventRecord(r.e, r.s) == hipSuccess))
             (void)hipEventSynchronize(r.e);
     for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket})
         if (b->p) (void)hipFree(b->p);
@@ -539,15 +542,15 @@ extern "C" int rxg_tcb_sync(rxg_ctx *c)
 }
 
 // Before a mirror write on c->stream: kernels that read the tables on other streams are
-// done.  The event is recorded now, on the reader's stream (it covers every launch the
+// done.  Lazy mode records the event now, on the reader's stream (it covers every launch the
 // stream has taken so far, the table readers among them).
 static int wait_table_readers(rxg_ctx *c)
 {
     for (auto &r : c->readers)
         if (r.pending) {
-            HIP_OK(hipEventRecord(r.e, r.s));
+            if (!r.recorded) HIP_OK(hipEventRecord(r.e, r.s));
             HIP_OK(hipStreamWaitEvent(c->stream, r.e, 0));
-            r.pending = false;
+            r.pending = r.recorded = false;
         }
     return 0;
 }
@@ -557,9 +560,9 @@ static int sync_table_readers(rxg_ctx *c)
 {
     for (auto &r : c->readers)
         if (r.pending) {
-            HIP_OK(hipEventRecord(r.e, r.s));
+            if (!r.recorded) HIP_OK(hipEventRecord(r.e, r.s));
             HIP_OK(hipEventSynchronize(r.e));
-            r.pending = false;
+            r.pending = r.recorded = false;
         }
     return 0;
 }
@@ -729,7 +732,7 @@ static int order_table_reader_after(rxg_ctx *c, hipStream_t st)
             // host's wait before a buffer is freed); no system-scope cache write-back
             hipEvent_t e;
             HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice));
-            c->readers.push_back({st, e, false, ~0ull});
+            c->readers.push_back({st, e, false, false, ~0ull});
             r = &c->readers.back();
         }
         // order_table_reader_before found no entry for st, so it has just waited for the
@@ -737,7 +740,13 @@ static int order_table_reader_after(rxg_ctx *c, hipStream_t st)
         r->waited = c->mirror_ev_set ? c->table_writes : ~0ull;
         r->s = st;
     }
-    r->pending = true;  // the event is recorded by the next write (wait_table_readers)
+    r->pending = true;
+    if (c->lazy_readers) {
+        r->recorded = false;  // recorded by the next write (wait_table_readers)
+    } else {
+        HIP_OK(hipEventRecord(r->e, st));
+        r->recorded = true;
+    }
     return 0;
 }
 

@@ -189,6 +189,7 @@ class HandoffOps(C.Structure):
 
 OPS_VERIFY_TCP_CKSUM = 0x1  # rxg_handoff_ops.flags: tcp_in.c:37-41 compiled in
 CFG_REPLAY_ON_DEVICE = 0x1  # rxg_config.flags: every replay fix-up is a GPU re-classify
+CFG_STREAMS_OUTLIVE_WRITES = 0x2  # caller streams stay valid until the next table write
 
 
 # ------------------------------------------------------------------------- loading ---

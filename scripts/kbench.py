@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--stream", action="store_true",
                     help="launch and time on a caller stream (a torch stream), not the context's own: "
                          "the table-reader ordering of DESIGN.md §2.4 runs per launch")
+    ap.add_argument("--engine-flags", type=int, default=0,
+                    help="rxg_config.flags of every variant's context (2 = RXG_CFG_STREAMS_OUTLIVE_WRITES)")
     ap.add_argument("--check", action="store_true",
                     help="also compare every variant's records (and counters) with the first variant's")
     args = ap.parse_args()
@@ -89,7 +91,7 @@ def main():
         # 6th field "arp": the ARP mirror on, loaded with every flow's source (ip.c:30-32 finds
         # them all: the kernel's ARP probe runs, RXG_F_ARP_LEARN stays clear)
         arp_on[v] = len(parts) > 5 and parts[5] == "arp"
-        engines[v] = rxg.Engine(0)
+        engines[v] = rxg.Engine(0, flags=args.engine_flags)
         rxg._lib = main_lib
     res = {(v, w): [] for v in engines for w in wls}
     for r in range(args.rounds):

@@ -154,11 +154,16 @@ def test_mirror_write_between_bursts_on_caller_streams(engine, second):
                 v.free()
 
 
-def test_mirror_write_waits_for_every_reader_stream(engine):
+@pytest.mark.parametrize("lazy", [False, True])
+def test_mirror_write_waits_for_every_reader_stream(lazy):
     """a long burst on s1, then a short one on s2, then removals, then a burst on
     the context's stream, with no host synchronisation in between.  The removals must wait
-    for BOTH readers (one event per reader stream, csrc/rxg_host.cpp order_table_reader_after):
-    the s1 burst classifies every frame against the old table."""
+    for BOTH readers (one entry per reader stream, csrc/rxg_host.cpp order_table_reader_after;
+    lazy = RXG_CFG_STREAMS_OUTLIVE_WRITES: the events recorded on the reader streams when the
+    write is pushed, wait_table_readers): the s1 burst classifies every frame against the old
+    table."""
+    engine = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20,
+                        flags=rxg.CFG_STREAMS_OUTLIVE_WRITES if lazy else 0)
     n, nflows, m = 1 << 20, 1000, 4096
     dev = engine.synth(n=n, nflows=nflows, len_a=1500, seed=78, with_flows=True)
     t0, l0 = rxg.synthetic_tcb_table(nflows)
@@ -189,6 +194,49 @@ def test_mirror_write_waits_for_every_reader_stream(engine):
     finally:
         for d in (out_a, out_s, out_c):
             d.free()
+        for v in dev.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()
+        engine.close()
+
+
+def test_caller_stream_destroyed_before_the_next_write(engine):
+    """rxg.h: without RXG_CFG_STREAMS_OUTLIVE_WRITES a caller stream that ran a burst may be
+    destroyed once synchronised, before the context's next table write: the write and the
+    next bursts still succeed and classify against the new table."""
+    import ctypes as C
+    # the HIP runtime this process already runs (librxg's and torch's), by its loaded path
+    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln)
+    hip = C.CDLL(path)
+    n, nflows = 1 << 16, 64
+    dev = engine.synth(n=n, nflows=nflows, len_a=64, seed=79, with_flows=True)
+    t0, l0 = rxg.synthetic_tcb_table(nflows)
+    flows = dev["flow"].download(np.uint32, n)
+    out = engine.alloc(n * 16)
+    try:
+        engine.tcb_load(t0, l0)
+        engine.tcb_sync()
+        for rep in range(3):
+            st = C.c_void_p()
+            assert hip.hipStreamCreate(C.byref(st)) == 0
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out.ptr, 16, st.value)
+            assert hip.hipStreamSynchronize(st) == 0
+            assert hip.hipStreamDestroy(st) == 0
+            a = out.download(rxg.REC16_DTYPE, n)
+            live = np.ones(nflows, dtype=bool)
+            live[: 2 * rep] = False
+            assert (a["tcb_idx"][live[flows]] == flows[live[flows]].astype(np.int32) + 1).all()
+            engine.tcb_remove(2 * rep + 1)       # flow 2 rep loses its TCB: a write
+            engine.tcb_remove(2 * rep + 2)
+            engine.tcb_sync()
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out.ptr, 16, None)
+            engine.sync()
+            c = out.download(rxg.REC16_DTYPE, n)
+            gone = flows < 2 * rep + 2
+            assert (c["tcb_idx"][~gone] == flows[~gone].astype(np.int32) + 1).all()
+            assert (c["tcb_idx"][gone] == 0).all()
+    finally:
+        out.free()
         for v in dev.values():
             if isinstance(v, rxg.DevArray):
                 v.free()
