@@ -2112,7 +2112,9 @@ __device__ __forceinline__ uint32_t srv_participants(uint32_t n)
     return max(1u, min(gridDim.x, (nsl + 3u) / 4u));
 }
 
-template <int MODE, int STRIP = 0>
+// SRVX (experiment builds, timing only: where a served burst's microseconds go): 1 = no rx
+// body (the protocol alone), 2 = no acquire at the request, 4 = no release before `done`
+template <int MODE, int STRIP = 0, int SRVX = 0>
 __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArgs sa)
 {
     __shared__ SrvReq s_req;
@@ -2153,7 +2155,7 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
             // (mirror tables, caller frames); waited for before any wave of the workgroup loads
             // (MI355X_MICROARCH.md, inter-workgroup visibility).  A first form with relaxed
             // polls and no acquire served stale staging lines (test_gpu_server).
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            if constexpr (!(SRVX & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             // the request's words, written by lanes 1-11, for lane 0
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2211,7 +2213,8 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
         a.b[0].n = uniform(s_req.n);
         a.b[0].slice0 = 0u;
         a.nslices = (a.b[0].n + 63u) / 64u;
-        rx_body<MODE, 0xFF, true, STRIP, false, 11, false, false, true, false, 0>(a, blockIdx.x, P);
+        if constexpr (!(SRVX & 1))
+            rx_body<MODE, 0xFF, true, STRIP, false, 11, false, false, true, false, 0>(a, blockIdx.x, P);
         // Every wave's stores have reached the L2 (vmcnt), then ONE system-scope release per
         // workgroup writes this XCD's L2 back (buffer_wbl2 covers the whole cache, so one
         // per workgroup covers its four waves; it used to run once per wave and once more
@@ -2219,7 +2222,7 @@ __global__ __launch_bounds__(256, (STRIP & 32768) ? 3 : 1) void rx_server(SrvArg
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            if constexpr (!(SRVX & 4)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bool lastp = true;
             if (P > 1u) {
@@ -2619,6 +2622,15 @@ hipError_t launch_server(const LaunchServer &L, hipStream_t st)
 #ifdef RXG_EXPERIMENTS
     if (L.variant == 78 && L.mode == 8) {  // the unpipelined body
         hipLaunchKernelGGL((rx_server<8, 0>), g, b, 0, st, sa);
+        return hipGetLastError();
+    }
+    if (L.variant >= 79 && L.variant <= 82 && L.mode == 8) {  // timing only: SRVX 1 / 2 / 4 / 6
+        switch (L.variant) {
+        case 79: hipLaunchKernelGGL((rx_server<8, 32768, 1>), g, b, 0, st, sa); break;
+        case 80: hipLaunchKernelGGL((rx_server<8, 32768, 2>), g, b, 0, st, sa); break;
+        case 81: hipLaunchKernelGGL((rx_server<8, 32768, 4>), g, b, 0, st, sa); break;
+        default: hipLaunchKernelGGL((rx_server<8, 32768, 6>), g, b, 0, st, sa); break;
+        }
         return hipGetLastError();
     }
 #endif
