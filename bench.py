@@ -445,10 +445,14 @@ def small_burst_leg(gpu, n=32, seconds=0.3):
             views = (rxg.PktView * n)(*[rxg.PktView(base + int(o) * 64, 0, int(ln), 0) for o, ln in zip(off, lens)])
             ptrs = (C.c_void_p * n)(*[base + int(o) * 64 for o in off])
 
+            # pointers taken once: numpy's .ctypes.data and C.byref cost ~2 us per call in
+            # Python, which the stack's own C loop does not pay
+            out_p, ops_r = out.ctypes.data, C.byref(ops)
+
             def one():
                 t = time.perf_counter()
-                assert lib.rxg_rx_burst(e.ctx, views, n, rxg.REC8, out.ctypes.data) == 0
-                assert lib.rxg_rx_replay(e.ctx, C.byref(ops), ptrs, ptrs, out.ctypes.data, n, rxg.REC8) == 0
+                assert lib.rxg_rx_burst(e.ctx, views, n, rxg.REC8, out_p) == 0
+                assert lib.rxg_rx_replay(e.ctx, ops_r, ptrs, ptrs, out_p, n, rxg.REC8) == 0
                 return time.perf_counter() - t
 
             def median_us():

@@ -50,7 +50,9 @@ def main():
     eng = rxg.Engine(0, max_batch=nmax, max_bytes=nmax * 1536)
     lib = rxg.load_library()
     out = np.zeros(nmax, dtype=rxg.REC8_DTYPE)
+    out_p = out.ctypes.data  # once: numpy's .ctypes.data costs ~2 us per access in Python
     ops = rxg.HandoffOps()
+    ops_r = C.byref(ops)
     for size in (64, 1500):
         b = eng.synth(n=nmax, nflows=1000, len_a=size, seed=99)
         eng.sync()
@@ -65,14 +67,17 @@ def main():
         d_out = eng.alloc(nmax * 8)
         for n in (1, 32, 256):
             def burst():
-                assert lib.rxg_rx_burst(eng.ctx, views, n, rxg.REC8, out.ctypes.data) == 0
+                assert lib.rxg_rx_burst(eng.ctx, views, n, rxg.REC8, out_p) == 0
 
             def burst_replay():
                 burst()
-                assert lib.rxg_rx_replay(eng.ctx, C.byref(ops), ptrs, ptrs, out.ctypes.data, n, rxg.REC8) == 0
+                assert lib.rxg_rx_replay(eng.ctx, ops_r, ptrs, ptrs, out_p, n, rxg.REC8) == 0
+
+            dbatch = rxg.DevBatch(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, rxg.REC8, d_out.ptr)
+            dref = C.byref(dbatch)  # built once, as the C loop would
 
             def dev():
-                eng.server_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, d_out.ptr, rxg.REC8)
+                assert lib.rxg_server_burst_dev(eng.ctx, dref) == 0
             row = {"frame_bytes": size, "n": n, "launched": per_call_us(burst_replay),
                    "launched_nr": per_call_us(burst)}
             for tag, flags in (("", 0), ("_hostmem", rxg.SRV_HOST_STAGING), ("_devmbox", rxg.SRV_DEVICE_MAILBOX)):
