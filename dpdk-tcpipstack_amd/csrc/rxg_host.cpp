@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstddef>
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
@@ -919,13 +920,30 @@ static int srv_post(rxg_ctx *c, const SrvReq &r)
     // stores may pass each other: each step is fenced (a no-op cost for host memory, whose
     // x86 stores are already visible in order).
     _mm_sfence();
-    S.mbox->req = r;
-    _mm_sfence();
     const unsigned long long q = ++S.seq;
-    __atomic_store_n(&S.mbox->seq2, q, __ATOMIC_RELEASE);
-    _mm_sfence();
-    __atomic_store_n(&S.mbox->seq, q, __ATOMIC_RELEASE);
-    _mm_sfence();
+    if (S.mdev) {
+        // Device mailbox (write-combined): the 128 bytes the server polls go out as two whole
+        // 64-byte lines (non-temporal 16-byte stores, one fence).  A line arrives whole, so
+        // the server, which takes a request only when seq (line 0) and seq2 (line 1) both
+        // show its number, sees either line old or both new with their request words.
+        alignas(64) unsigned long long head[16] = {};
+        static_assert(sizeof(SrvReq) + 8 <= offsetof(SrvMbox, seq2), "mailbox head layout");
+        head[0] = q;
+        std::memcpy(&head[1], &r, sizeof(SrvReq));
+        head[offsetof(SrvMbox, seq2) / 8] = q;
+        head[offsetof(SrvMbox, stop) / 8] = 0ull;
+        const __m128i *src = reinterpret_cast<const __m128i *>(head);
+        __m128i *dst = reinterpret_cast<__m128i *>(S.mbox);
+        for (int i = 0; i < 8; ++i) _mm_stream_si128(dst + i, _mm_load_si128(src + i));
+        _mm_sfence();
+    } else {
+        S.mbox->req = r;
+        _mm_sfence();
+        __atomic_store_n(&S.mbox->seq2, q, __ATOMIC_RELEASE);
+        _mm_sfence();
+        __atomic_store_n(&S.mbox->seq, q, __ATOMIC_RELEASE);
+        _mm_sfence();
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spins = 1;; ++spins) {
         if (__atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE) == q) break;
