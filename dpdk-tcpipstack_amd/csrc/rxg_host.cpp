@@ -204,13 +204,13 @@ struct rxg_ctx {
 
     // latency-mode server (rxg_server_*): a persistent kernel on its own
     // stream; the host-burst staging in device memory the host writes through the BAR
-    // (dev = true) or in coherent host memory; the mailbox, answers and records in host
-    // memory (the mailbox in device memory only with RXG_SRV_DEVICE_MAILBOX)
+    // (dev = true) or in coherent host memory; the mailbox likewise (mdev), answers and
+    // records in host memory
     struct Server {
         bool on = false;        // configured (the kernel may have exited idle: relaunched on demand)
         bool launched = false;  // a kernel was launched since the last stream synchronisation
         bool dev = false;       // arena / off / len in device memory (host writes only)
-        bool mdev = false;      // mbox in device memory (RXG_SRV_DEVICE_MAILBOX)
+        bool mdev = false;      // mbox in device memory (large BAR, no RXG_SRV_HOST_MAILBOX)
         hipStream_t st = nullptr;
         SrvMbox *mbox = nullptr;  // host-written words: seq, request, stop
         SrvMbox *ret = nullptr;   // server-written words: done, exited (host memory; = mbox if !mdev)
@@ -1017,13 +1017,13 @@ extern "C" int rxg_server_start(rxg_ctx *c, const rxg_server_config *cfg)
     // Placement: with a large BAR the host writes the staged frames and
     // descriptors into fine-grained device memory (posted PCIe writes) and the server reads
     // them from HBM; otherwise they are coherent host memory the server reads over PCIe.  The
-    // mailbox stays in host memory unless RXG_SRV_DEVICE_MAILBOX.
+    // mailbox follows unless RXG_SRV_HOST_MAILBOX (written as two whole lines, srv_post).
     int large_bar = 0;
     if (!(cfg->flags & RXG_SRV_HOST_STAGING) &&
         hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) != hipSuccess)
         large_bar = 0;
     S.dev = large_bar != 0;
-    S.mdev = S.dev && (cfg->flags & RXG_SRV_DEVICE_MAILBOX);
+    S.mdev = S.dev && !(cfg->flags & RXG_SRV_HOST_MAILBOX);
     const unsigned flags = hipHostMallocCoherent | hipHostMallocMapped;
     auto place = [&](bool dev, void **p, size_t bytes) {
         return dev ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained) == hipSuccess

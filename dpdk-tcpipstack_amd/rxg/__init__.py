@@ -34,7 +34,7 @@ F_IP_OK, F_TCP_OK, F_LISTEN, F_REF_NULLSLOT, F_TRUNC, F_ARP_LEARN = 1, 2, 4, 8, 
 REC8, REC16, REC48 = 8, 16, 48
 # rxg_server_config.flags and rxg_server_placement (include/rxg.h)
 SRV_HOST_STAGING = 1
-SRV_DEVICE_MAILBOX = 2
+SRV_HOST_MAILBOX = 2
 SRV_NONE, SRV_HOST, SRV_DEVICE = 0, 1, 2
 
 COUNTERS = ["rx", "bytes", "ipv4", "arp", "other_l2", "tcp", "non_tcp", "ip_cksum_bad",

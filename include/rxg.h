@@ -384,8 +384,8 @@ int rxg_rx_burst(rxg_ctx *ctx, const rxg_pkt_view *pkts, uint32_t n, uint32_t re
    PCIe trips of its frames and records.  The host-burst staging (frames, descriptors)
    lives in device memory the host writes through the PCIe BAR (posted writes; the server
    reads HBM) when the device exposes its memory to the host (large BAR), else in coherent
-   host memory (RXG_SRV_HOST_STAGING forces that); the mailbox is coherent host memory the
-   server polls (RXG_SRV_DEVICE_MAILBOX moves it to device memory too, measured slower);
+   host memory (RXG_SRV_HOST_STAGING forces that); the mailbox the server polls is device
+   memory too on such a device (RXG_SRV_HOST_MAILBOX keeps it in coherent host memory);
    the server's answers and the records of host bursts are written to host memory.
    While the server runs,
    rxg_rx_burst sends bursts of up to max_frames frames (max_bytes staged bytes) and of
@@ -403,7 +403,7 @@ typedef struct rxg_server_config {
     uint32_t flags;       /* RXG_SRV_*; 0 = mailbox and staging placed by the device */
 } rxg_server_config;
 #define RXG_SRV_HOST_STAGING 1u   /* staging in coherent host memory */
-#define RXG_SRV_DEVICE_MAILBOX 2u /* mailbox in device memory (large BAR only) */
+#define RXG_SRV_HOST_MAILBOX 2u   /* mailbox in coherent host memory */
 int rxg_server_start(rxg_ctx *ctx, const rxg_server_config *cfg);
 /* Stops the server and waits for its kernel to end; 0 if none runs. */
 int rxg_server_stop(rxg_ctx *ctx);

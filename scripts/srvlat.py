@@ -10,7 +10,7 @@
 The served columns are measured for both placements of the mailbox and staging, one after
 the other in the same process: "device" staging (device memory the host writes through the
 BAR, the default on a large-BAR GPU), "_hostmem" (RXG_SRV_HOST_STAGING, coherent host memory)
-and "_devmbox" (RXG_SRV_DEVICE_MAILBOX: the mailbox in device memory too).
+and "_hostmbox" (RXG_SRV_HOST_MAILBOX: device staging, the mailbox in host memory).
 
 python scripts/srvlat.py [--blocks 4]   (one JSON line per frame size and burst)"""
 import argparse
@@ -80,7 +80,7 @@ def main():
                 assert lib.rxg_server_burst_dev(eng.ctx, dref) == 0
             row = {"frame_bytes": size, "n": n, "launched": per_call_us(burst_replay),
                    "launched_nr": per_call_us(burst)}
-            for tag, flags in (("", 0), ("_hostmem", rxg.SRV_HOST_STAGING), ("_devmbox", rxg.SRV_DEVICE_MAILBOX)):
+            for tag, flags in (("", 0), ("_hostmem", rxg.SRV_HOST_STAGING), ("_hostmbox", rxg.SRV_HOST_MAILBOX)):
                 eng.server_start(rxg.REC8, blocks=args.blocks, max_frames=nmax, flags=flags)
                 row["placement" + tag] = {rxg.SRV_DEVICE: "device", rxg.SRV_HOST: "host"}[eng.server_placement()]
                 row.update({"served" + tag: per_call_us(burst_replay), "served_nr" + tag: per_call_us(burst),

@@ -133,7 +133,7 @@ def test_server_config_layout_matches_header():
 int main(void) {
   printf("%zu %zu %zu %zu %u %u %d %d %d\n", sizeof(rxg_server_config), offsetof(rxg_server_config, max_bytes),
          offsetof(rxg_server_config, idle_ms), offsetof(rxg_server_config, flags), RXG_SRV_HOST_STAGING,
-         RXG_SRV_DEVICE_MAILBOX, RXG_SRV_NONE, RXG_SRV_HOST, RXG_SRV_DEVICE);
+         RXG_SRV_HOST_MAILBOX, RXG_SRV_NONE, RXG_SRV_HOST, RXG_SRV_DEVICE);
   return 0;
 }'''
     tmp = os.path.join(ROOT, "build_abi_probe")
@@ -145,7 +145,7 @@ int main(void) {
     got = subprocess.run([os.path.join(tmp, "srv")], capture_output=True, text=True, check=True).stdout.split()
     assert [int(x) for x in got] == [C.sizeof(rxg.ServerConfig), rxg.ServerConfig.max_bytes.offset,
                                      rxg.ServerConfig.idle_ms.offset, rxg.ServerConfig.flags.offset,
-                                     rxg.SRV_HOST_STAGING, rxg.SRV_DEVICE_MAILBOX, rxg.SRV_NONE, rxg.SRV_HOST,
+                                     rxg.SRV_HOST_STAGING, rxg.SRV_HOST_MAILBOX, rxg.SRV_NONE, rxg.SRV_HOST,
                                      rxg.SRV_DEVICE]
 
 

@@ -26,7 +26,7 @@ def srv_engine():
 
 # rxg_server_config.flags: 0 = placed by the device (device memory on a large-BAR GPU),
 # SRV_HOST_STAGING = coherent host memory
-PLACEMENTS = [0, rxg.SRV_HOST_STAGING, rxg.SRV_DEVICE_MAILBOX]
+PLACEMENTS = [0, rxg.SRV_HOST_STAGING, rxg.SRV_HOST_MAILBOX]
 
 
 def test_server_placement_reported(srv_engine):
