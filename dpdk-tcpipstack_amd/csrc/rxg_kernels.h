@@ -73,7 +73,9 @@ struct SrvReq {
     uint32_t flags;          // reserved (0)
     DevTable table;          // the mirror as of the post
 };
-// Coherent host memory.  The first 128 bytes are what the host writes and the server polls,
+// Device memory written through the BAR (large-BAR GPUs, two whole lines per post) or coherent
+// host memory; `done` / `exited` are read from the server's return block (host memory, may
+// be a second SrvMbox).  The first 128 bytes are what the host writes and the server polls,
 // read whole by one wave instruction (16 lanes x 8 bytes): a request is taken when seq and
 // seq2 both show its number (the host writes req, then seq2, then seq; each 64-byte line is
 // read as one snapshot, so both numbers new means every field of both lines is new).  The
