@@ -544,6 +544,45 @@ def cpu_replicas(arena, off, lens, tcb, live, cores, seconds):
             "sample": f"{cores} processes, frames split {cuts[1] - cuts[0]}-ish each, {seconds:.1f} s"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(ngpus: int) -> int:
+    """`python bench.py --gpus N` (N > 1) with no launcher around it: start N fresh rank
+    processes through torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) as a
+    CHILD process and return its exit code.  Nothing here touches the GPU (device_count does
+    not initialise it on this image), and the parent never execs.  The ranks are this same
+    script with the same arguments; they see WORLD_SIZE and run main's rank path."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ngpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")  # torch.distributed.run's own default, without its warning
+    return subprocess.run(cmd, env=env).returncode
+
+
+def rank_devices(gpu: int, have_gpu: bool, device) -> list:
+    """Every rank's device as the rank itself sees it (gathered to all ranks): what the line's
+    n_gpus / ranks were measured on."""
+    me = {"rank": int(os.environ.get("RANK", 0)), "device": f"cuda:{gpu}" if have_gpu else "cpu"}
+    if have_gpu:
+        p = torch.cuda.get_device_properties(gpu)
+        me["name"] = p.name
+        uuid = getattr(p, "uuid", None)
+        if uuid is not None:
+            me["uuid"] = str(uuid)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [me]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -563,16 +602,45 @@ def main():
                     help="weak: --frames per GPU; strong: --total-frames split over the GPUs")
     ap.add_argument("--total-frames", type=int, default=1 << 23)
     args = ap.parse_args()
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus {args.gpus}: need at least 1")
 
-    rank, world, local = rank_env()
     # RXG_BENCH_REHEARSE=1: rehearse N ranks on fewer GPUs (device = local_rank mod #GPUs,
     # gloo backend for the collectives) -- a correctness rehearsal, never a measurement.
     rehearse = os.environ.get("RXG_BENCH_REHEARSE") == "1"
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            ndev = torch.cuda.device_count()
+            if not rehearse and ndev < args.gpus:
+                sys.exit(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible "
+                         "(RXG_BENCH_REHEARSE=1 rehearses more ranks than GPUs)")
+            sys.exit(spawn_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: launched with WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}")
+
+    rank, world, local = rank_env()
+    have_gpu = torch.cuda.device_count() > 0
     gpu = local % max(1, torch.cuda.device_count()) if rehearse else local
     if world > 1:
-        torch.cuda.set_device(gpu)
+        if have_gpu:
+            torch.cuda.set_device(gpu)
         dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
-    device = torch.device("cpu") if (rehearse and world > 1) else torch.device("cuda", gpu)
+    device = torch.device("cpu") if (rehearse and world > 1) or not have_gpu else torch.device("cuda", gpu)
+    ranks = dist.get_world_size() if dist.is_initialized() else 1
+    devices = rank_devices(gpu, have_gpu, device)
+    if not have_gpu:
+        if not rehearse:
+            sys.exit("bench.py: no GPU visible")
+        # rehearsal on a host without a GPU: the launcher, the rendezvous and the collectives
+        # only; nothing is measured, so the line carries no value
+        t = max_over_ranks(float(rank + 1), device)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "ranks": ranks,
+                              "devices": devices, "rehearsal": "no GPU: launcher, rendezvous and collectives only",
+                              "max_over_ranks_check": t}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     torch.cuda.set_device(gpu)
     eng = rxg.Engine(device=gpu)
     stream = None  # the engine's own stream
@@ -675,6 +743,10 @@ def main():
             "unit": "GB/s",
             "mpps": round(mpps, 2),
             "n_gpus": world,
+            "ranks": ranks,
+            "devices": devices,
+            "distinct_devices": len({d.get("uuid", d["device"]) for d in devices}),
+            "collective_backend": dist.get_backend() if dist.is_initialized() else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),

@@ -26,6 +26,7 @@
 #include "rxg_mirror.h"
 #include "rxg_opqueue.h"
 #include "rxg_packpool.h"
+#include "rxg_srvfsm.h"
 
 using namespace rxg;
 
@@ -59,6 +60,18 @@ extern "C" const char *rxg_last_error(void) { return g_err; }
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
+};
+
+// The latency-mode server's device side as rxg::SrvFsm sees it (rxg_srvfsm.h); defined
+// after rxg_ctx.
+struct SrvPort {
+    rxg_ctx *c;
+    unsigned long long done() const;
+    bool exited() const;
+    void write(unsigned long long q);
+    void request_stop();
+    int launch();
+    void sync();
 };
 
 struct rxg_ctx {
@@ -131,6 +144,7 @@ struct rxg_ctx {
     bool touched_pass2 = false;          // min_null moved (the pass-2 NULL-slot flag)
     bool replay_on_device = false;       // RXG_CFG_REPLAY_ON_DEVICE
     bool lazy_readers = false;           // RXG_CFG_STREAMS_OUTLIVE_WRITES
+    std::vector<hipStream_t> registered; // that mode's caller streams (rxg_stream_register)
     uint64_t rp_stats[4] = {0, 0, 0, 0}; // marked, host fix-ups, device fix-ups, launches
 
     // the last burst's device batch (re-classification reads it again)
@@ -163,9 +177,6 @@ struct rxg_ctx {
     std::vector<uint32_t> rcv_cur;
     std::vector<uint8_t> rcv_state;
     DevBuf d_pg_status, d_pg_ticket;
-#ifdef RXG_EXPERIMENTS
-    DevBuf d_exp_hdr;  // RXG_VARIANT 21: contiguous header lines of a tx batch
-#endif
     unsigned long long pg_tickets = 0;  // workgroups the gathers have launched so far
     uint32_t pg_epoch = 0;
     rxg_payload_msg *h_pm = nullptr;
@@ -208,7 +219,8 @@ struct rxg_ctx {
     // records in host memory
     struct Server {
         bool on = false;        // configured (the kernel may have exited idle: relaunched on demand)
-        bool launched = false;  // a kernel was launched since the last stream synchronisation
+        rxg::SrvFsm<SrvPort> fsm;  // Down / Up / Failed (rxg_srvfsm.h)
+        SrvReq req{};           // the request SrvPort::write posts
         bool dev = false;       // arena / off / len in device memory (host writes only)
         bool mdev = false;      // mbox in device memory (large BAR, no RXG_SRV_HOST_MAILBOX)
         hipStream_t st = nullptr;
@@ -355,9 +367,6 @@ extern "C" int rxg_fini(rxg_ctx *c)
             (void)hipEventSynchronize(r.e);
     for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket})
         if (b->p) (void)hipFree(b->p);
-#ifdef RXG_EXPERIMENTS
-    if (c->d_exp_hdr.p) (void)hipFree(c->d_exp_hdr.p);
-#endif
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
     for (auto &pb : c->patch) {
@@ -698,9 +707,20 @@ static int arp_sync(rxg_ctx *c)
 
 // A launch on `st` that reads the mirror tables: it follows the last mirror write, and
 // the next mirror write follows it.
+static bool stream_registered(const rxg_ctx *c, hipStream_t st)
+{
+    return std::find(c->registered.begin(), c->registered.end(), st) != c->registered.end();
+}
+
 static int order_table_reader_before(rxg_ctx *c, hipStream_t st)
 {
-    if (st == c->stream || !c->mirror_ev_set) return 0;
+    if (st == c->stream) return 0;
+    // RXG_CFG_STREAMS_OUTLIVE_WRITES: the next write records an event on `st`, so `st` must
+    // still exist then; only a registered stream is known to (rxg_stream_retire ends that)
+    if (c->lazy_readers && !stream_registered(c, st))
+        return fail(-EINVAL, "table-reading launch on stream %p, not registered with rxg_stream_register "
+                             "(RXG_CFG_STREAMS_OUTLIVE_WRITES)", (void *)st);
+    if (!c->mirror_ev_set) return 0;
     // a stream that already waited for the current mirror_ev needs no second wait (each wait
     // is a barrier packet between the caller's launches)
     for (auto &x : c->readers)
@@ -748,6 +768,36 @@ static int order_table_reader_after(rxg_ctx *c, hipStream_t st)
         HIP_OK(hipEventRecord(r->e, st));
         r->recorded = true;
     }
+    return 0;
+}
+
+extern "C" int rxg_stream_register(rxg_ctx *c, void *stream)
+{
+    if (!c || !stream) return fail(-EINVAL, "rxg_stream_register: NULL argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (st != c->stream && !stream_registered(c, st)) c->registered.push_back(st);
+    return 0;
+}
+
+extern "C" int rxg_stream_retire(rxg_ctx *c, void *stream)
+{
+    if (!c || !stream) return fail(-EINVAL, "rxg_stream_retire: NULL argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (st == c->stream) return 0;
+    int rc = set_device(c);
+    if (rc) return rc;
+    // the order the next table write needs against this stream's launches, taken now; the
+    // entry then names no stream (a new stream may get the same handle)
+    for (auto &r : c->readers)
+        if (r.s == st) {
+            if (r.pending && !r.recorded) {
+                HIP_OK(hipEventRecord(r.e, st));
+                r.recorded = true;
+            }
+            r.s = nullptr;
+            r.waited = ~0ull;
+        }
+    c->registered.erase(std::remove(c->registered.begin(), c->registered.end(), st), c->registered.end());
     return 0;
 }
 
@@ -829,6 +879,22 @@ static int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bur
     return 0;
 }
 
+// A receive launch: the product kernels, or in the experiment library the ablation kernels
+// of RXG_VARIANT (rxg_kernels_exp.hip).
+static hipError_t rx_launch(const rxg_ctx *c, const LaunchRx &L, hipStream_t st)
+{
+#ifdef RXG_EXPERIMENTS
+    if (c->variant) {
+        LaunchRx X = L;
+        X.variant = c->variant;
+        return launch_rx_exp(X, st);
+    }
+#else
+    (void)c;
+#endif
+    return launch_rx(L, st);
+}
+
 static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
                          void *stream, const char *who)
 {
@@ -840,7 +906,7 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
     for (uint32_t j0 = 0; j0 < k; j0 += kMaxBursts) {
         const uint32_t m = std::min(kMaxBursts, k - j0);
         for (uint32_t j = 0; j < m; ++j)
-            lb[j] = LaunchBurst{bursts[j0 + j].off64, bursts[j0 + j].len, bursts[j0 + j].n, (uint8_t *)bursts[j0 + j].out};
+            lb[j] = LaunchBurst{bursts[j0 + j].off64, bursts[j0 + j].len, bursts[j0 + j].n, (uint8_t *)bursts[j0 + j].out, 0u};
         LaunchRx L;
         std::memset(&L, 0, sizeof L);
         L.frames = (const uint8_t *)frames;
@@ -852,8 +918,7 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
         L.max_blocks = c->max_blocks ? c->max_blocks : (rec_kind == RXG_REC48 ? c->grid_rec48
                                                         : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
         if (L.max_blocks == 0) L.max_blocks = 1024;
-        L.variant = c->variant;
-        HIP_OK(launch_rx(L, st));
+        HIP_OK(rx_launch(c, L, st));
     }
     if ((rc = order_table_reader_after(c, st))) return rc;
     c->burst_ok = true;
@@ -877,89 +942,93 @@ extern "C" int rxg_rx_bursts_dev(rxg_ctx *c, const void *frames, const rxg_dev_b
 }
 
 // ---------------------------------------------------------------- latency mode ---
-// (Re)launch the server kernel.  A previous kernel has left its loop (stop / idle) or was
-// never launched; its stream is synchronised before the mailbox and control words reset.
-static int srv_launch(rxg_ctx *c)
+// (Re)launch the server kernel.  A previous kernel has left its loop (stop / idle) or none
+// ran (the state machine synchronised its stream first); the mailbox's stop, the return
+// block's exited and the control words are reset before the launch.
+int SrvPort::launch()
 {
     rxg_ctx::Server &S = c->srv;
-    if (S.launched) {
-        HIP_OK(hipStreamSynchronize(S.st));
-        S.launched = false;
-    }
     __atomic_store_n(&S.mbox->stop, 0ull, __ATOMIC_RELEASE);  // plain stores: no locked op over the BAR
     __atomic_store_n(&S.ret->exited, 0ull, __ATOMIC_SEQ_CST);
     _mm_sfence();  // device memory is write-combined on the host
     SrvCtl init;
     std::memset(&init, 0, sizeof init);
-    init.go = __atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE);  // the workgroups wait past it
+    init.go = __atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE) << 16;  // the workgroups wait past it
     HIP_OK(hipMemcpyAsync(S.ctl, &init, sizeof init, hipMemcpyHostToDevice, S.st));
     HIP_OK(hipStreamSynchronize(S.st));
     LaunchServer L;
     L.mbox = S.mbox;
     L.ret = S.ret;
     L.ctl = S.ctl;
-    L.counters = c->counters;
+    L.counters = c->nocount ? nullptr : c->counters;
     L.idle_ticks = S.idle_ticks;
     L.blocks = S.blocks;
     L.mode = (int)S.rec_kind;
+#ifdef RXG_EXPERIMENTS
     L.variant = c->variant;
+    if (c->variant >= 79 && c->variant <= 82) {
+        HIP_OK(launch_server_exp(L, S.st));
+        return 0;
+    }
+#endif
     HIP_OK(launch_server(L, S.st));
-    S.launched = true;
     return 0;
 }
 
-// Post one request and wait for its `done`.  A kernel that exited idle before it saw the
-// request is relaunched; the new one starts from `done` and serves it.
-static int srv_post(rxg_ctx *c, const SrvReq &r)
+unsigned long long SrvPort::done() const { return __atomic_load_n(&c->srv.ret->done, __ATOMIC_ACQUIRE); }
+bool SrvPort::exited() const { return __atomic_load_n(&c->srv.ret->exited, __ATOMIC_ACQUIRE) != 0ull; }
+void SrvPort::sync() { (void)hipStreamSynchronize(c->srv.st); }
+void SrvPort::request_stop()
+{
+    __atomic_store_n(&c->srv.mbox->stop, 1ull, __ATOMIC_RELEASE);
+    _mm_sfence();
+}
+
+// Post request q (S.req).  The staging is fenced before the request (device memory is
+// write-combined on the host, where stores may pass each other).  The server takes the
+// request when seq is new and the check word matches seq and the request words (SrvMbox):
+// whatever order or pieces the mailbox's lines reach it in, it never runs a request with
+// another's words.
+void SrvPort::write(unsigned long long q)
 {
     rxg_ctx::Server &S = c->srv;
-    int rc;
-    if ((!S.launched || __atomic_load_n(&S.ret->exited, __ATOMIC_ACQUIRE)) && (rc = srv_launch(c))) return rc;
-    // the staging, the request, then seq2, then seq (the server takes the request when it
-    // reads both numbers new, SrvMbox).  Device memory is write-combined on the host, where
-    // stores may pass each other: each step is fenced (a no-op cost for host memory, whose
-    // x86 stores are already visible in order).
     _mm_sfence();
-    const unsigned long long q = ++S.seq;
+    const unsigned long long ck = srv_check(q, S.req);
     if (S.mdev) {
         // Device mailbox (write-combined): the 128 bytes the server polls go out as two whole
-        // 64-byte lines (non-temporal 16-byte stores, one fence).  A line arrives whole, so
-        // the server, which takes a request only when seq (line 0) and seq2 (line 1) both
-        // show its number, sees either line old or both new with their request words.
+        // 64-byte lines (non-temporal 16-byte stores, one fence).
         alignas(64) unsigned long long head[16] = {};
-        static_assert(sizeof(SrvReq) + 8 <= offsetof(SrvMbox, seq2), "mailbox head layout");
+        static_assert(sizeof(SrvReq) + 8 <= offsetof(SrvMbox, check), "mailbox head layout");
         head[0] = q;
-        std::memcpy(&head[1], &r, sizeof(SrvReq));
-        head[offsetof(SrvMbox, seq2) / 8] = q;
+        std::memcpy(&head[1], &S.req, sizeof(SrvReq));
+        head[offsetof(SrvMbox, check) / 8] = ck;
         head[offsetof(SrvMbox, stop) / 8] = 0ull;
         const __m128i *src = reinterpret_cast<const __m128i *>(head);
         __m128i *dst = reinterpret_cast<__m128i *>(S.mbox);
         for (int i = 0; i < 8; ++i) _mm_stream_si128(dst + i, _mm_load_si128(src + i));
         _mm_sfence();
     } else {
-        S.mbox->req = r;
-        _mm_sfence();
-        __atomic_store_n(&S.mbox->seq2, q, __ATOMIC_RELEASE);
-        _mm_sfence();
+        S.mbox->req = S.req;
+        __atomic_store_n(&S.mbox->check, ck, __ATOMIC_RELEASE);
         __atomic_store_n(&S.mbox->seq, q, __ATOMIC_RELEASE);
         _mm_sfence();
     }
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint64_t spins = 1;; ++spins) {
-        if (__atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE) == q) break;
-        __builtin_ia32_pause();
-        if ((spins & 1023u) == 0u) {
-            if (__atomic_load_n(&S.ret->exited, __ATOMIC_ACQUIRE)) {
-                if (__atomic_load_n(&S.ret->done, __ATOMIC_ACQUIRE) == q) break;
-                if ((rc = srv_launch(c))) return rc;
-            }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
-                __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_RELEASE);
-                _mm_sfence();
-                return fail(-ETIMEDOUT, "rxg_server: request %llu not served in 10 s", q);
-            }
-        }
-    }
+}
+
+// Post one request and wait for its `done` (rxg_srvfsm.h: relaunch after an idle exit, 10 s
+// limit, -EIO while a kernel that missed its limit is still resident).
+static int srv_post(rxg_ctx *c, const SrvReq &r)
+{
+    rxg_ctx::Server &S = c->srv;
+    S.req = r;
+    SrvPort port{c};
+    const unsigned long long q = S.fsm.seq + 1u;
+    const int rc = S.fsm.post(port);
+    if (rc == -ETIMEDOUT)
+        return fail(rc, "rxg_server: request %llu not served in 10 s (the server is stopping; until its kernel "
+                        "exits, requests fail with -EIO)", q);
+    if (rc == -EIO) return fail(rc, "rxg_server: a kernel that missed its time limit has not exited");
+    if (rc) return fail(rc, "rxg_server: launch failed");
     return 0;
 }
 
@@ -982,15 +1051,13 @@ extern "C" int rxg_server_stop(rxg_ctx *c)
     if (!c->srv.on) return 0;
     int rc = set_device(c);
     if (rc) return rc;
-    rxg_ctx::Server &S = c->srv;
-    hipError_t e = hipSuccess;
-    if (S.launched) {
-        __atomic_store_n(&S.mbox->stop, 1ull, __ATOMIC_RELEASE);
-        _mm_sfence();
-        e = hipStreamSynchronize(S.st);
+    SrvPort port{c};
+    if (c->srv.fsm.stop(port)) {
+        // the kernel is still resident and may still write the staging: nothing is freed
+        // (a later stop, or rxg_fini, tries again)
+        return fail(-EIO, "rxg_server_stop: the server kernel has not exited");
     }
     srv_free(c);
-    if (e != hipSuccess) return fail(-EIO, "rxg_server_stop: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -1049,9 +1116,10 @@ extern "C" int rxg_server_start(rxg_ctx *c, const rxg_server_config *cfg)
         std::memset(S.mbox, 0, sizeof(SrvMbox));
     }
     S.on = true;
-    if ((rc = srv_launch(c))) {
+    SrvPort port{c};
+    if ((rc = S.fsm.relaunch(port))) {
         srv_free(c);
-        return rc;
+        return fail(rc, "rxg_server_start: launch failed");
     }
     return 0;
 }
@@ -1106,13 +1174,7 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
         return fail(-EINVAL, "rxg_tx_cksum_dev: frames need 16-byte, off64 4-byte, len 2-byte alignment");
     int rc = set_device(c);
     if (rc) return rc;
-    LaunchBurst one{b->off64, b->len, b->n, nullptr};
-#ifdef RXG_EXPERIMENTS
-    if (c->variant == 21) {
-        if ((rc = ensure(c->d_exp_hdr, (size_t)b->n * 64u))) return rc;
-        one.out = (uint8_t *)c->d_exp_hdr.p;
-    }
-#endif
+    LaunchBurst one{b->off64, b->len, b->n, nullptr, 0u};
     LaunchRx L;
     std::memset(&L, 0, sizeof L);
     L.frames = (const uint8_t *)b->frames;
@@ -1120,7 +1182,6 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
     L.nbursts = 1;
     L.mode = 0;
     L.counters = nullptr;
-    L.variant = c->variant;
     L.max_blocks = c->max_blocks ? c->max_blocks : c->grid_tx;
     if (L.max_blocks == 0) L.max_blocks = 1024;
     HIP_OK(launch_rx(L, pick(c, stream)));
@@ -1452,7 +1513,7 @@ static int reclassify(rxg_ctx *c, const std::vector<uint32_t> &sel, std::vector<
     if ((rc = ensure(c->d_fix, sel.size() * sizeof(rxg_rec16)))) return rc;
     if (c->dirty && (rc = tcb_push(c))) return rc;
     HIP_OK(hipMemcpyAsync(c->d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, c->stream));
-    const LaunchBurst one{c->last_off, c->last_len, (uint32_t)sel.size(), (uint8_t *)c->d_fix.p};
+    const LaunchBurst one{c->last_off, c->last_len, (uint32_t)sel.size(), (uint8_t *)c->d_fix.p, 0u};
     LaunchRx L;
     std::memset(&L, 0, sizeof L);
     L.frames = c->last_frames;

@@ -12,10 +12,11 @@ namespace rxg {
 // burst k's frame i is at frames + 64 * off64[i], its record at out + i * record size.
 constexpr uint32_t kMaxBursts = 32;
 struct LaunchBurst {
-    const uint32_t *off64;
+    const uint32_t *off64;  // strided launches (LaunchRx::stride64 != 0): unused
     const uint16_t *len;
     uint32_t n;            // >= 1 (empty bursts are not launched)
     uint8_t *out;          // records (receive), unused for tx
+    uint32_t slot0;        // strided launches: the 64-byte slot of the burst's frame 0
 };
 
 struct LaunchRx {
@@ -27,7 +28,8 @@ struct LaunchRx {
     DevTable table;
     unsigned long long *counters;
     uint32_t max_blocks;   // grid cap (grid-stride over 64-frame slices)
-    int variant;           // 0 = production kernel; >0 = experiment variants (RXG_VARIANT)
+    uint32_t stride64;     // nonzero: frame i of a burst at slot slot0 + i * stride64 (no off64[])
+    int variant;           // experiment library only (launch_rx_exp): RXG_VARIANT
 };
 
 struct LaunchSynth {
@@ -59,6 +61,11 @@ struct LaunchPayload {
 };
 
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
+#ifdef RXG_EXPERIMENTS
+// rxg_kernels_exp.hip (experiment library only): the ablation kernels of L.variant;
+// hipErrorInvalidValue for a variant it does not know
+hipError_t launch_rx_exp(const LaunchRx &L, hipStream_t st);
+#endif
 
 // Latency mode (rxg_server_*): a persistent set of workgroups that classifies one burst after
 // another.  The host posts a request in a mailbox of fine-grained (coherent) host memory and
@@ -76,27 +83,48 @@ struct SrvReq {
 // Device memory written through the BAR (large-BAR GPUs, two whole lines per post) or coherent
 // host memory; `done` / `exited` are read from the server's return block (host memory, may
 // be a second SrvMbox).  The first 128 bytes are what the host writes and the server polls,
-// read whole by one wave instruction (16 lanes x 8 bytes): a request is taken when seq and
-// seq2 both show its number (the host writes req, then seq2, then seq; each 64-byte line is
-// read as one snapshot, so both numbers new means every field of both lines is new).  The
-// server's words are on a line of their own.
+// read whole by one wave instruction (16 lanes x 8 bytes): a request is taken when seq is new
+// and `check` is srv_check of seq and the request words.  Write-combined stores reach the
+// device as whole lines or in parts, in any order between lines until the host's fence: the
+// check word is what makes a snapshot holding words of two requests fail (it is then polled
+// again), not the order of the stores.  The server's words are on a line of their own.
 struct alignas(128) SrvMbox {
     unsigned long long seq;       // host: number of the request posted
     SrvReq req;
-    unsigned long long seq2;      // host: = seq, written after req
+    unsigned long long check;     // host: srv_check(seq, req)
     unsigned long long stop;      // host: nonzero = exit
     unsigned long long hpad[1];
     alignas(128) unsigned long long done;  // server: number of the last request finished
     unsigned long long exited;    // server: nonzero once the kernel has left its loop
 };
 static_assert(sizeof(SrvReq) == 88, "mailbox layout");
-static_assert(offsetof(SrvMbox, seq2) == 96 && offsetof(SrvMbox, stop) == 104 && offsetof(SrvMbox, done) == 128,
+static_assert(offsetof(SrvMbox, check) == 96 && offsetof(SrvMbox, stop) == 104 && offsetof(SrvMbox, done) == 128,
               "mailbox layout");
+// Word i (0 = seq, 1-11 = the request) of the mailbox mixed with its position; the check word
+// is the XOR of the twelve (a splitmix64 finaliser: any mix of old and new words changes it
+// but with probability 2^-64).
+__host__ __device__ inline unsigned long long srv_mix(unsigned i, unsigned long long w)
+{
+    unsigned long long z = w + (unsigned long long)(i + 1u) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+inline unsigned long long srv_check(unsigned long long seq, const SrvReq &r)
+{
+    unsigned long long w[sizeof(SrvReq) / 8];
+    __builtin_memcpy(w, &r, sizeof w);
+    unsigned long long h = srv_mix(0u, seq);
+    for (unsigned i = 0; i < sizeof(SrvReq) / 8; ++i) h ^= srv_mix(i + 1u, w[i]);
+    return h;
+}
 struct SrvCtl {                   // device memory
-    unsigned long long go;        // the request the workgroups run (kSrvStop: exit)
-    unsigned int fin;             // workgroups finished, all requests (monotonic)
+    unsigned long long go;        // number << 16 | participants of the request the workgroups run
+                                  // (kSrvStop: exit); the host sets done << 16 before a launch
+    unsigned int fin;             // participants finished with the current request (the last
+                                  // one resets it to 0 before publishing `done`)
     unsigned int pad;
-    SrvReq req;
+    SrvReq req;                   // the current request, read by its participants only
 };
 constexpr unsigned long long kSrvStop = ~0ull;
 struct LaunchServer {
@@ -107,9 +135,12 @@ struct LaunchServer {
     unsigned long long idle_ticks;  // wall-clock ticks without a request before the kernel exits
     uint32_t blocks;
     int mode;                       // record kind 8 / 16 / 48
-    int variant;                    // 0 = production; experiment variants (RXG_VARIANT)
+    int variant;                    // experiment library only (launch_server_exp): RXG_VARIANT
 };
 hipError_t launch_server(const LaunchServer &L, hipStream_t st);
+#ifdef RXG_EXPERIMENTS
+hipError_t launch_server_exp(const LaunchServer &L, hipStream_t st);  // rxg_kernels_exp.hip
+#endif
 // rxg_payload.hip: gather of the burst's candidate payloads (one launch + a memset)
 hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *tickets_used);
 uint32_t payload_blocks(uint32_t n);

@@ -219,6 +219,8 @@ def load_library(path: str = LIB_PATH):
         "rxg_fini": (C.c_int, [vp]),
         "rxg_sync": (C.c_int, [vp]),
         "rxg_stream": (vp, [vp]),
+        "rxg_stream_register": (C.c_int, [vp, vp]),
+        "rxg_stream_retire": (C.c_int, [vp, vp]),
         "rxg_tcb_upsert": (C.c_int, [vp, i32, C.POINTER(TcbTuple)]),
         "rxg_tcb_remove": (C.c_int, [vp, i32]),
         "rxg_tcb_set_state": (C.c_int, [vp, i32, C.c_uint8]),
@@ -471,6 +473,14 @@ class Engine:
 
     def sync(self):
         _check(_lib.rxg_sync(self.ctx), "rxg_sync")
+
+    def stream_register(self, stream: int):
+        """rxg_stream_register: a caller stream of a CFG_STREAMS_OUTLIVE_WRITES context."""
+        _check(_lib.rxg_stream_register(self.ctx, stream), "rxg_stream_register")
+
+    def stream_retire(self, stream: int):
+        """rxg_stream_retire: the stream may be destroyed after this."""
+        _check(_lib.rxg_stream_retire(self.ctx, stream), "rxg_stream_retire")
 
     def host_register(self, a: np.ndarray) -> int:
         """Page-lock and map a host array for zero-copy batches; returns its device alias."""

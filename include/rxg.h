@@ -209,12 +209,14 @@ typedef struct rxg_config {
 /* rxg_config.flags.  RXG_CFG_REPLAY_ON_DEVICE: rxg_rx_replay re-classifies every packet a
    handler's tcbs[] write affects with a GPU launch (the default answers small sets from the
    host index the device mirror is patched from; same records either way).
-   RXG_CFG_STREAMS_OUTLIVE_WRITES: the caller promises that every stream it passes to a
-   table-reading launch stays valid until the context's next table write or rxg_fini (it is
-   not destroyed in between, even after a synchronisation).  The write's order against those
-   launches is then taken when the write is pushed (an event recorded on the stream then)
+   RXG_CFG_STREAMS_OUTLIVE_WRITES: the write's order against table-reading launches on
+   caller streams is taken when the write is pushed (an event recorded on the stream then)
    instead of by a marker after every launch, which on a caller stream cost ~4.5 us per
-   launch.  Without the flag a stream may be destroyed once synchronised. */
+   launch.  The recording needs the stream to exist at the write, so in this
+   mode a caller stream must be registered (rxg_stream_register) before its first
+   table-reading launch (rxg_rx_burst_dev, rxg_rx_bursts_dev; else -EINVAL, nothing
+   launched) and retired (rxg_stream_retire) before it is destroyed.  Without the flag a
+   stream may be destroyed once synchronised. */
 #define RXG_CFG_REPLAY_ON_DEVICE 0x1u
 #define RXG_CFG_STREAMS_OUTLIVE_WRITES 0x2u
 
@@ -226,6 +228,13 @@ int rxg_fini(rxg_ctx *ctx);
 int rxg_sync(rxg_ctx *ctx);
 /* The hipStream_t rxg launches on when a NULL stream is passed. */
 void *rxg_stream(rxg_ctx *ctx);
+/* Caller streams of a RXG_CFG_STREAMS_OUTLIVE_WRITES context (any context accepts them).
+   register: `stream` may carry table-reading launches from now on.  retire: the context
+   takes, now, the order its next table write needs against the stream's launches and forgets
+   the stream; the caller may then destroy it.  The context's own stream needs neither.
+   0, or -EINVAL for a NULL argument. */
+int rxg_stream_register(rxg_ctx *ctx, void *stream);
+int rxg_stream_retire(rxg_ctx *ctx, void *stream);
 
 /* ------------------------------------------------------------------------- */
 /* TCB mirror.  The reference mutates `tcbs[]` directly (tcp_tcb.c:21-22,     */

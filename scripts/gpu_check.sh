@@ -6,8 +6,8 @@
 #   pytest      the whole -m gpu suite
 #   smoke       __graft_entry__.smoke()
 #   bench       the default bench line (bench.json)
-#   rehearse    bench.py with 2 ranks on the box's one GPU (gloo collectives; a rehearsal,
-#               never a scaling figure)
+#   rehearse    bench.py --gpus 2 (bench.py spawns its 2 ranks itself) on the box's one GPU
+#               (gloo collectives; a rehearsal, never a scaling figure)
 #   prof        rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes per workload
 #               (scripts/gpu_prof.sh; PROF_WLS, default "c3 c4 c2 c2multi"; REC, default 8)
 #   sq          SQ counter passes per workload (scripts/gpu_sq.sh; SQ_WLS)
@@ -39,8 +39,7 @@ for S in "$@"; do
     pytest)    step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke)     step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)     step bench 500 python -u bench.py; cp "$OUT/bench.log" "$OUT/bench.json" ;;
-    rehearse)  step rehearse2 600 env RXG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
-                 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 3 ;;
+    rehearse)  step rehearse2 600 env RXG_BENCH_REHEARSE=1 python3 -u bench.py --gpus 2 --steps 20 --warmup 3 ;;
     prof)      step prof 900 env REC=${REC:-8} bash scripts/gpu_prof.sh "$TAG/prof" ${PROF_WLS:-c3 c4 c2 c2multi} ;;
     sq)        step sq 600 env REC=${REC:-8} bash scripts/gpu_sq.sh ${SQ_WLS:-c4 c3} ;;
     ab)        step ab 800 env TAG="$TAG/ab" bash scripts/gpu_ab.sh ;;

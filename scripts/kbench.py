@@ -92,6 +92,8 @@ def main():
         # them all: the kernel's ARP probe runs, RXG_F_ARP_LEARN stays clear)
         arp_on[v] = len(parts) > 5 and parts[5] == "arp"
         engines[v] = rxg.Engine(0, flags=args.engine_flags)
+        if st is not None and hasattr(lib, "rxg_stream_register"):  # (older builds: no such call)
+            engines[v].stream_register(st)  # needed by RXG_CFG_STREAMS_OUTLIVE_WRITES contexts
         rxg._lib = main_lib
     res = {(v, w): [] for v in engines for w in wls}
     for r in range(args.rounds):

@@ -177,22 +177,33 @@ EXPERIMENT_SWITCHES = [b"RXG_VARIANT", b"RXG_NOCOUNT", b"RXG_PG_VARIANT", b"RXG_
 
 
 def _kernel_instantiations(path):
-    """(MODE, CMASK, NT, STRIP) of every rx_kernel in the library's gfx950 code object."""
+    """(MODE, DESC, MULTI, DEEP, ABL) of every rx_kernel in the library's gfx950 code object
+    (csrc/rxg_rx.h: rx_kernel<MODE, DESC, MULTI, DEEP, ABL>)."""
     data = open(path, "rb").read()
-    return set(re.findall(rb"rx_kernelILi(\d+)ELi(\d+)ELb(\d)ELi(\d+)E", data))
+    return {tuple(int(x) for x in m) for m in
+            re.findall(rb"rx_kernelILi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELi(\d+)EEEv", data)}
+
+
+# The product kernels: round 3's set (every record kind single / multi-burst, the two-deep
+# REC8 / REC16 forms, tx, the REC16 re-classification through a selection list) plus the
+# fixed-stride REC8 / REC16 forms (DESC 2).
+PRODUCT_KERNELS = ({(m, 0, mu, dp, 0) for m in (8, 16) for mu in (0, 1) for dp in (0, 1)}
+                   | {(m, 2, mu, dp, 0) for m in (8, 16) for mu in (0, 1) for dp in (0, 1)}
+                   | {(48, 0, 0, 0, 0), (48, 0, 1, 0, 0), (0, 0, 0, 0, 0), (16, 1, 0, 0, 0)})
 
 
 def test_product_library_has_no_experiment_switches():
     """librxg.so reads no environment variable that changes what a burst computes and holds
-    only the production kernels: every rx_kernel handles every size class (CMASK 255) and
-    strips nothing (STRIP 0).  The variants live in the experiment build (librxg_exp.so,
-    make experiments) that scripts/kbench.py and pgbench.py load."""
+    only the production kernels: no ablation (ABL 0 everywhere), exactly PRODUCT_KERNELS.
+    The ablation kernels live in the experiment build (librxg_exp.so, make experiments,
+    csrc/rxg_kernels_exp.hip) that scripts/kbench.py loads."""
     data = open(rxg.LIB_PATH, "rb").read()
     for sw in EXPERIMENT_SWITCHES:
         assert sw not in data, sw
     inst = _kernel_instantiations(rxg.LIB_PATH)
-    assert inst, "no rx_kernel found in the code object"
-    assert all(cmask == b"255" and strip == b"0" for _, cmask, _, strip in inst), inst
+    assert inst == PRODUCT_KERNELS, sorted(inst ^ PRODUCT_KERNELS)
+    servers = set(re.findall(rb"rx_serverILi(\d+)ELi(\d+)EEEv", data))
+    assert servers == {(b"8", b"0"), (b"16", b"0"), (b"48", b"0")}, servers
     assert re.findall(rb"pg_gather", data)
 
 
@@ -202,7 +213,20 @@ def test_experiment_library_is_separate():
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "dpdk-tcpipstack_amd"), "experiments"], check=True)
     data = open(exp, "rb").read()
     assert all(sw in data for sw in EXPERIMENT_SWITCHES)
-    assert any(strip != b"0" for _, _, _, strip in _kernel_instantiations(exp))
+    inst = _kernel_instantiations(exp)
+    assert PRODUCT_KERNELS <= inst and any(abl != 0 for *_, abl in inst)
+
+
+def test_kernel_source_has_no_experiment_branches():
+    """the product kernel source keeps no experiment scaffolding: no
+    RXG_EXPERIMENTS blocks, no STRIP bits, and rx_body takes at most 6 template parameters."""
+    csrc = os.path.join(ROOT, "dpdk-tcpipstack_amd", "csrc")
+    for f in ("rxg_kernels.hip", "rxg_rx.h"):
+        src = open(os.path.join(csrc, f)).read()
+        assert "RXG_EXPERIMENTS" not in src and "STRIP" not in src, f
+    body = open(os.path.join(csrc, "rxg_rx.h")).read()
+    m = re.search(r"template <([^>]*)>\s*__device__ __forceinline__ void rx_body\(", body)
+    assert m and len(m.group(1).split(",")) <= 6, m and m.group(1)
 
 
 def test_handoff_ops_layout_matches_header():

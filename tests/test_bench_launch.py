@@ -1,0 +1,51 @@
+"""bench.py's own launcher: `python bench.py --gpus N`
+with no launcher around it starts N rank processes itself, and the line reports how many
+ranks the collectives saw.  Here (no GPU) through the rehearsal mode: the same spawn, the
+same rendezvous and gloo collectives, no measurement."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "MASTER_ADDR", "MASTER_PORT")}
+    env["HIP_VISIBLE_DEVICES"] = env.get("HIP_VISIBLE_DEVICES", "")
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _lines(out):
+    return [json.loads(s) for s in out.splitlines() if s.startswith("{")]
+
+
+def test_gpus_2_spawns_two_ranks():
+    r = _run(["--gpus", "2", "--no-legs", "--no-cpu"], {"RXG_BENCH_REHEARSE": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["ranks"] == 2
+    assert sorted(d["rank"] for d in line["devices"]) == [0, 1]
+    assert line["max_over_ranks_check"] == 2.0  # the gloo all-reduce saw both ranks
+
+
+def test_gpus_1_is_one_process():
+    r = _run(["--gpus", "1", "--no-legs", "--no-cpu"], {"RXG_BENCH_REHEARSE": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _lines(r.stdout)
+    assert line["n_gpus"] == 1 and line["ranks"] == 1 and len(line["devices"]) == 1
+
+
+def test_world_size_disagreeing_with_gpus_fails():
+    r = _run(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_more_gpus_than_visible_fails_without_rehearsal():
+    r = _run(["--gpus", "2"])
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr

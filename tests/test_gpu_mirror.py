@@ -170,6 +170,8 @@ def test_mirror_write_waits_for_every_reader_stream(lazy):
     flows = dev["flow"].download(np.uint32, n)
     out_a, out_s, out_c = engine.alloc(n * 16), engine.alloc(m * 16), engine.alloc(n * 16)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for st in (s1, s2):  # required in the lazy mode, harmless otherwise
+        engine.stream_register(st.cuda_stream)
     try:
         for _ in range(3):
             engine.tcb_load(t0, l0)
@@ -200,14 +202,20 @@ def test_mirror_write_waits_for_every_reader_stream(lazy):
         engine.close()
 
 
-def test_caller_stream_destroyed_before_the_next_write(engine):
-    """rxg.h: without RXG_CFG_STREAMS_OUTLIVE_WRITES a caller stream that ran a burst may be
-    destroyed once synchronised, before the context's next table write: the write and the
-    next bursts still succeed and classify against the new table."""
+@pytest.mark.parametrize("lazy", [False, True])
+def test_caller_stream_destroyed_before_the_next_write(lazy):
+    """rxg.h: a caller stream that ran a burst may be destroyed before the context's next table
+    write: once synchronised without RXG_CFG_STREAMS_OUTLIVE_WRITES, once retired
+    (rxg_stream_retire) with it.  The write and the next bursts still succeed and classify
+    against the new table.  With the flag, a launch on an unregistered stream is refused with
+    -EINVAL and launches nothing (round 3 crashed in tcb_sync: an event recorded on a stream
+    destroyed before the write, gpurun_out/r03s3l/pytest_mirror.txt)."""
     import ctypes as C
     # the HIP runtime this process already runs (librxg's and torch's), by its loaded path
     path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln)
     hip = C.CDLL(path)
+    engine = rxg.Engine(device=0, max_batch=1 << 16, max_bytes=64 << 20,
+                        flags=rxg.CFG_STREAMS_OUTLIVE_WRITES if lazy else 0)
     n, nflows = 1 << 16, 64
     dev = engine.synth(n=n, nflows=nflows, len_a=64, seed=79, with_flows=True)
     t0, l0 = rxg.synthetic_tcb_table(nflows)
@@ -219,8 +227,16 @@ def test_caller_stream_destroyed_before_the_next_write(engine):
         for rep in range(3):
             st = C.c_void_p()
             assert hip.hipStreamCreate(C.byref(st)) == 0
+            if lazy:
+                with pytest.raises(rxg.RxgError, match="not registered"):
+                    engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out.ptr, 16, st.value)
+            engine.stream_register(st.value)
             engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out.ptr, 16, st.value)
+            if lazy:
+                engine.stream_retire(st.value)   # before the synchronisation: the order is taken now
             assert hip.hipStreamSynchronize(st) == 0
+            if not lazy:
+                engine.stream_retire(st.value)   # accepted either way
             assert hip.hipStreamDestroy(st) == 0
             a = out.download(rxg.REC16_DTYPE, n)
             live = np.ones(nflows, dtype=bool)
@@ -240,3 +256,4 @@ def test_caller_stream_destroyed_before_the_next_write(engine):
         for v in dev.values():
             if isinstance(v, rxg.DevArray):
                 v.free()
+        engine.close()
