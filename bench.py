@@ -44,7 +44,10 @@ TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.jso
                  ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r03/final/c2multi/traffic.json",
                  # the 8(f) kernels over the headline's C3 batch (scripts/gpu_prof.sh tx3 / pg3)
                  ("tx_generate_dev", 1 << 20, 8): "profiles/r03/final/tx3/traffic.json",
-                 ("payload_gather", 1 << 20, 8): "profiles/r03/final/pg3/traffic.json"}
+                 ("payload_gather", 1 << 20, 8): "profiles/r03/final/pg3/traffic.json",
+                 # round 4: the fixed-stride forms (rxg_rx_bursts_strided_dev), scripts/gpu_prof.sh c2s c2multis
+                 ("c2_64B_1flow_strided", 1 << 20, 8): "profiles/r04/c2s/traffic.json",
+                 ("c2_64B_1flow_multiburst_strided", 1 << 20, 8): "profiles/r04/c2multis/traffic.json"}
 
 
 def traffic_of(name, n, rec):
@@ -130,10 +133,14 @@ class Workload:
         self.bytes_per_batch = int(self.lens.astype(np.uint64).sum())
         self.out = eng.alloc(n * rec)
 
-    def launch(self, eng, i, stream=None):
+    def launch(self, eng, i, stream=None, strided=False):
         b = self.batches[i % self.copies]
-        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, self.n, self.out.ptr,
-                         self.rec, stream)
+        if strided:  # rxg_rx_bursts_strided_dev: fixed-size frames, frame i at slot i * slots
+            eng.rx_bursts_strided_dev(b["arena"].ptr, (self.frame_len + 63) // 64,
+                                      [(0, b["len"].ptr, self.n, self.out.ptr)], self.rec, stream)
+        else:
+            eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, self.n, self.out.ptr,
+                             self.rec, stream)
 
     def free(self):
         for b in self.batches:
@@ -143,9 +150,9 @@ class Workload:
         self.out.free()
 
 
-def time_workload(eng, wl, steps, warmup, device, stream):
+def time_workload(eng, wl, steps, warmup, device, stream, strided=False):
     for i in range(warmup):
-        wl.launch(eng, i, stream)
+        wl.launch(eng, i, stream, strided)
     eng.sync()
     eng.counters_reset()
     evs = [(eng.event(), eng.event()) for _ in range(steps)]
@@ -153,7 +160,7 @@ def time_workload(eng, wl, steps, warmup, device, stream):
     t0 = time.perf_counter()
     for i in range(steps):
         eng.record(evs[i][0], stream)
-        wl.launch(eng, warmup + i, stream)
+        wl.launch(eng, warmup + i, stream, strided)
         eng.record(evs[i][1], stream)
     eng.sync()
     barrier(device)
@@ -165,7 +172,7 @@ def time_workload(eng, wl, steps, warmup, device, stream):
     return elapsed, kern_ms
 
 
-def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=rxg.REC16):
+def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=rxg.REC16, strided=False):
     """C2 (configs[1]: 2^20 x 64 B, 1 flow) as a ring of `nbursts` distinct 2^20-frame bursts
     in one 1 GiB frame pool (the same working set as the rotating C2 leg, beyond the 256 MB
     Infinity Cache), classified by ONE launch (rxg_rx_bursts_dev) instead of one launch per
@@ -177,9 +184,17 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=
     out = eng.alloc(n * nbursts * rec)
     bursts = [(pool["off64"].ptr + j * n * 4, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * rec)
               for j in range(nbursts)]
+    # strided: the same frames through rxg_rx_bursts_strided_dev (burst j's frame i at slot j n + i)
+    sbursts = [(j * n, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * rec) for j in range(nbursts)]
+
+    def launch():
+        if strided:
+            eng.rx_bursts_strided_dev(pool["arena"].ptr, 1, sbursts, rec)
+        else:
+            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
     try:
         for _ in range(warmup):
-            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
+            launch()
         eng.sync()
         eng.counters_reset()
         evs = [(eng.event(), eng.event()) for _ in range(steps)]
@@ -187,7 +202,7 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=
         t0 = time.perf_counter()
         for a, b in evs:
             eng.record(a)
-            eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
+            launch()
             eng.record(b)
         eng.sync()
         barrier(device)
@@ -200,7 +215,9 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=
         if rec == rxg.REC8:
             last = rxg.rec8_expand(last)
         return {"bursts_per_launch": nbursts, "frames_per_burst": n, "rec_kind": rec,
-                "traffic_bytes_per_launch": traffic_of("c2_64B_1flow_multiburst", n, rec)[0],
+                "descriptors": "fixed stride (no off64[])" if strided else "off64[] + len[]",
+                "traffic_bytes_per_launch": traffic_of("c2_64B_1flow_multiburst" + ("_strided" if strided else ""),
+                                                       n, rec)[0],
                 "algorithmic_bytes_per_launch": alg,
                 "kernel_us_per_launch": round(k * 1e6, 2), "kernel_us_per_burst": round(k * 1e6 / nbursts, 2),
                 "mpps": round(frames_all / dt / 1e6, 2), "gbs": round(frames_all * 64 / dt / 1e9, 2),
@@ -686,13 +703,14 @@ def main():
         legs[f"{args.workload}_rec{other}"] = {"kernel_us": round(ka * 1e6, 2),
                                                "roofline_frac": round(ow.bytes_per_batch / ka / 1e9 / HBM_PEAK_GBS, 4)}
         ow.free()
-        for name in ("c2_64B_1flow", "c4_imix_64Kflows"):
-            if name == args.workload:
+        for name, strided in (("c2_64B_1flow", False), ("c2_64B_1flow_strided", True), ("c4_imix_64Kflows", False)):
+            wname = name.replace("_strided", "")
+            if wname == args.workload:
                 continue
-            lw = Workload(eng, name, frames, seed + 99, args.rec)
+            lw = Workload(eng, wname, frames, seed + 99, args.rec)
             t2, l2 = rxg.synthetic_tcb_table(lw.flows)
             eng.tcb_load(t2, l2)
-            e2, k2 = time_workload(eng, lw, args.steps, args.warmup, device, stream)
+            e2, k2 = time_workload(eng, lw, args.steps, args.warmup, device, stream, strided)
             e2 = max_over_ranks(e2, device)
             c2 = merge_counters(eng.counters(), device)
             ka = float(np.mean(k2)) / 1e3
@@ -706,12 +724,15 @@ def main():
                 "working_set_GiB": round(lw.copies * (lw.batches[0]["arena_bytes"]) / 2**30, 3),
                 "counters_ok": bool(int(c2[0]) == ln
                                     and int(c2[7]) == 0 and int(c2[8]) == 0),
+                "descriptors": "fixed stride (no off64[])" if strided else "off64[] + len[]",
                 "traffic_bytes_per_launch": traffic_of(name, lw.n, args.rec)[0],
                 "algorithmic_bytes_per_launch": lw.bytes_per_batch,
             }
             lw.free()
         legs["c2_64B_1flow_multiburst"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed,
                                                          rec=args.rec)
+        legs["c2_64B_1flow_multiburst_strided"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device, seed,
+                                                                 rec=args.rec, strided=True)
         # the other record kind on the same ring
         legs[f"c2_64B_1flow_multiburst_rec{other}"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device,
                                                                      seed, rec=other)

@@ -151,10 +151,11 @@ struct rxg_ctx {
     // The last launch's bursts (one, or several of one frame pool: rxg_rx_bursts_dev) and
     // the one a replay / gather refers to next (last_off .. last_recs below).
     struct BurstRef {
-        const uint32_t *off64;
+        const uint32_t *off64;  // nullptr for a fixed-stride burst (slot0, stride64)
         const uint16_t *len;
         uint32_t n;
         const uint8_t *recs;
+        uint32_t slot0 = 0, stride64 = 0;
     };
     std::vector<BurstRef> last_bursts;
     uint32_t replay_cursor = 0;
@@ -164,7 +165,11 @@ struct rxg_ctx {
     std::vector<int32_t> launch_listen;
     bool launch_all = false, launch_pass2 = false;
     const uint8_t *last_frames = nullptr;
-    const uint32_t *last_off = nullptr;
+    const uint32_t *last_off = nullptr;  // nullptr: a fixed-stride burst (burst_offsets)
+    uint32_t last_slot0 = 0, last_stride64 = 0;
+    DevBuf d_soff;                       // a fixed-stride burst's offsets, written on demand
+    uint32_t soff_slot0 = 0, soff_stride64 = 0, soff_n = 0;  // what d_soff holds (n 0: nothing),
+    hipStream_t soff_stream = nullptr;                        // written on this stream
     const uint16_t *last_len = nullptr;
     uint32_t last_n = 0;
     bool burst_ok = false;  // the last burst was launched (device) / completed (host buffers)
@@ -365,7 +370,8 @@ extern "C" int rxg_fini(rxg_ctx *c)
     for (auto &r : c->readers)  // table readers still running on caller streams
         if (r.pending && (r.recorded || hipEventRecord(r.e, r.s) == hipSuccess))
             (void)hipEventSynchronize(r.e);
-    for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket})
+    for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket,
+                      &c->d_soff})
         if (b->p) (void)hipFree(b->p);
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
@@ -821,6 +827,8 @@ static void select_burst(rxg_ctx *c, uint32_t j)
     c->replay_cursor = j;
     const rxg_ctx::BurstRef &b = c->last_bursts[j];
     c->last_off = b.off64;
+    c->last_slot0 = b.slot0;
+    c->last_stride64 = b.stride64;
     c->last_len = b.len;
     c->last_n = b.n;
     c->last_recs = b.recs;
@@ -832,8 +840,10 @@ static void select_burst(rxg_ctx *c, uint32_t j)
 static bool rec_kind_ok(uint32_t k) { return k == RXG_REC8 || k == RXG_REC16 || k == RXG_REC48; }
 
 // Validation, mirror sync and the replay bookkeeping of a burst set (launched or served).
+// stride64 != 0: fixed-stride bursts (rxg_rx_bursts_strided_dev): bursts[j].off64 is unused and
+// bursts[j].pad holds the burst's first slot.
 static int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
-                        const char *who)
+                        const char *who, uint32_t stride64 = 0)
 {
     // a rejected launch leaves nothing to replay: rxg_rx_replay refuses until a burst succeeds
     c->burst_ok = false;
@@ -846,8 +856,10 @@ static int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bur
     const uintptr_t rec_align = rec_kind == RXG_REC8 ? 8u : 16u;
     for (uint32_t j = 0; j < k; ++j) {
         if (!bursts[j].n) continue;
-        if (!bursts[j].off64 || !bursts[j].len || !bursts[j].out)
+        if ((!stride64 && !bursts[j].off64) || !bursts[j].len || !bursts[j].out)
             return fail(-EINVAL, "%s: NULL device pointer in burst %u", who, j);
+        if (stride64 && (uint64_t)bursts[j].pad + (uint64_t)(bursts[j].n - 1u) * stride64 > 0xFFFFFFFFull)
+            return fail(-EINVAL, "%s: burst %u: slot0 + (n - 1) * stride64 exceeds 2^32 - 1 slots", who, j);
         if (((uintptr_t)bursts[j].off64 & 3u) || ((uintptr_t)bursts[j].len & 1u) ||
             ((uintptr_t)bursts[j].out & (rec_align - 1u)))
             return fail(-EINVAL, "%s: burst %u: off64 needs 4-byte, len 2-byte, out %u-byte alignment", who, j,
@@ -866,7 +878,8 @@ static int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bur
     c->last_stride = rec_kind;
     c->last_bursts.clear();
     for (uint32_t j = 0; j < k; ++j)
-        c->last_bursts.push_back({bursts[j].off64, bursts[j].len, bursts[j].n, (const uint8_t *)bursts[j].out});
+        c->last_bursts.push_back({stride64 ? nullptr : bursts[j].off64, bursts[j].len, bursts[j].n,
+                                  (const uint8_t *)bursts[j].out, stride64 ? bursts[j].pad : 0u, stride64});
     if (c->last_bursts.empty()) c->last_bursts.push_back({nullptr, nullptr, 0u, nullptr});
     select_burst(c, 0);
     // the records reflect the mirror as of now: changes are tracked from here (replay)
@@ -896,9 +909,9 @@ static hipError_t rx_launch(const rxg_ctx *c, const LaunchRx &L, hipStream_t st)
 }
 
 static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
-                         void *stream, const char *who)
+                         void *stream, const char *who, uint32_t stride64 = 0)
 {
-    int rc = begin_bursts(c, frames, bursts, k, rec_kind, who);
+    int rc = begin_bursts(c, frames, bursts, k, rec_kind, who, stride64);
     if (rc) return rc;
     hipStream_t st = pick(c, stream);
     if ((rc = order_table_reader_before(c, st))) return rc;
@@ -906,7 +919,8 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
     for (uint32_t j0 = 0; j0 < k; j0 += kMaxBursts) {
         const uint32_t m = std::min(kMaxBursts, k - j0);
         for (uint32_t j = 0; j < m; ++j)
-            lb[j] = LaunchBurst{bursts[j0 + j].off64, bursts[j0 + j].len, bursts[j0 + j].n, (uint8_t *)bursts[j0 + j].out, 0u};
+            lb[j] = LaunchBurst{stride64 ? nullptr : bursts[j0 + j].off64, bursts[j0 + j].len, bursts[j0 + j].n,
+                                (uint8_t *)bursts[j0 + j].out, stride64 ? bursts[j0 + j].pad : 0u};
         LaunchRx L;
         std::memset(&L, 0, sizeof L);
         L.frames = (const uint8_t *)frames;
@@ -914,6 +928,7 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
         L.nbursts = m;
         L.mode = (int)rec_kind;
         L.table = table_view(c);
+        L.stride64 = stride64;
         L.counters = c->nocount ? nullptr : c->counters;
         L.max_blocks = c->max_blocks ? c->max_blocks : (rec_kind == RXG_REC48 ? c->grid_rec48
                                                         : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
@@ -939,6 +954,40 @@ extern "C" int rxg_rx_bursts_dev(rxg_ctx *c, const void *frames, const rxg_dev_b
 {
     if (!c) return fail(-EINVAL, "rxg_rx_bursts_dev: ctx NULL");
     return launch_bursts(c, frames, bursts, k, rec_kind, stream, "rxg_rx_bursts_dev");
+}
+
+extern "C" int rxg_rx_bursts_strided_dev(rxg_ctx *c, const void *frames, uint32_t stride64,
+                                         const rxg_dev_strided_burst *bursts, uint32_t k, uint32_t rec_kind,
+                                         void *stream)
+{
+    if (!c) return fail(-EINVAL, "rxg_rx_bursts_strided_dev: ctx NULL");
+    if (!stride64) return fail(-EINVAL, "rxg_rx_bursts_strided_dev: stride64 0");
+    if (k && !bursts) return fail(-EINVAL, "rxg_rx_bursts_strided_dev: NULL burst table");
+    std::vector<rxg_dev_burst> b(k);
+    for (uint32_t j = 0; j < k; ++j) b[j] = rxg_dev_burst{nullptr, bursts[j].len, bursts[j].n, bursts[j].slot0, bursts[j].out};
+    return launch_bursts(c, frames, b.data(), k, rec_kind, stream, "rxg_rx_bursts_strided_dev", stride64);
+}
+
+// The selected burst's offsets as a device array: its own off64, or for a fixed-stride burst
+// slot0 + i * stride64 written into d_soff on `st` (the payload gather and the re-classify
+// launch read offsets through a list; rare for strided bursts, which exist for the bulk path).
+static int burst_offsets(rxg_ctx *c, hipStream_t st, const uint32_t **out)
+{
+    *out = c->last_off;
+    if (c->last_off || !c->last_stride64) return 0;
+    // (rewritten for a reader on another stream: the same values, ordered on the reader's stream)
+    if (c->soff_n != c->last_n || c->soff_slot0 != c->last_slot0 || c->soff_stride64 != c->last_stride64 ||
+        c->soff_stream != st) {
+        int rc = ensure(c->d_soff, (size_t)c->last_n * 4u);
+        if (rc) return rc;
+        HIP_OK(launch_strided_offsets((uint32_t *)c->d_soff.p, c->last_n, c->last_slot0, c->last_stride64, st));
+        c->soff_n = c->last_n;
+        c->soff_slot0 = c->last_slot0;
+        c->soff_stride64 = c->last_stride64;
+        c->soff_stream = st;
+    }
+    *out = (const uint32_t *)c->d_soff.p;
+    return 0;
 }
 
 // ---------------------------------------------------------------- latency mode ---
@@ -1339,7 +1388,7 @@ extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void
     c->pg_epoch = (c->pg_epoch % ((1u << 30) - 1u)) + 1u;
     LaunchPayload P;
     P.frames = c->last_frames;
-    P.off64 = c->last_off;
+    if ((rc = burst_offsets(c, st, &P.off64))) return rc;
     P.len = c->last_len;
     P.recs = c->last_recs;
     P.stride = c->last_stride;
@@ -1507,13 +1556,15 @@ static void host_classify(const rxg_ctx *c, const uint8_t *f, rxg_rec16 &r)
 static int reclassify(rxg_ctx *c, const std::vector<uint32_t> &sel, std::vector<rxg_rec16> &out)
 {
     int rc;
-    if (!c->last_frames || !c->last_off || !c->last_len)
+    const uint32_t *off64 = nullptr;
+    if ((rc = burst_offsets(c, c->stream, &off64))) return rc;
+    if (!c->last_frames || !off64 || !c->last_len)
         return fail(-EINVAL, "rxg_rx_replay: no burst on this context to re-classify against");
     if ((rc = ensure(c->d_sel, sel.size() * 4))) return rc;
     if ((rc = ensure(c->d_fix, sel.size() * sizeof(rxg_rec16)))) return rc;
     if (c->dirty && (rc = tcb_push(c))) return rc;
     HIP_OK(hipMemcpyAsync(c->d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, c->stream));
-    const LaunchBurst one{c->last_off, c->last_len, (uint32_t)sel.size(), (uint8_t *)c->d_fix.p, 0u};
+    const LaunchBurst one{off64, c->last_len, (uint32_t)sel.size(), (uint8_t *)c->d_fix.p, 0u};
     LaunchRx L;
     std::memset(&L, 0, sizeof L);
     L.frames = c->last_frames;

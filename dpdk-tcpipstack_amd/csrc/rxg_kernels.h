@@ -147,6 +147,8 @@ uint32_t payload_blocks(uint32_t n);
 // resident 256-thread workgroups per CU of the production kernel of `mode`
 int rx_blocks_per_cu(int mode);
 hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);
+// off[i] = slot0 + i * stride64, i < n (a fixed-stride burst's offsets as a list)
+hipError_t launch_strided_offsets(uint32_t *off, uint32_t n, uint32_t slot0, uint32_t stride64, hipStream_t st);
 // rxg_mirror.h patches (n of them, host-visible memory) applied to the device mirror tables
 struct MirrorPatch;
 // Replay counter corrections (two's complement: a negative delta wraps the uint64 sum)

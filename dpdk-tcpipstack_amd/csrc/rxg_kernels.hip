@@ -5,6 +5,7 @@
 // the ablation kernels are rxg_kernels_exp.hip, built into librxg_exp.so only.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
 
@@ -157,9 +158,12 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     switch (L.mode) {
     case 8: strided ? launch_mode<8, kDescStride>(a, g, st) : launch_mode<8, kDescList>(a, g, st); break;
     case 16: strided ? launch_mode<16, kDescStride>(a, g, st) : launch_mode<16, kDescList>(a, g, st); break;
-    case 48:
-        if (strided) return hipErrorInvalidValue;
-        if (a.nbursts > 1)
+    case 48:  // (never two-deep: 48-byte records are the inspection form, not the bulk one)
+        if (strided && a.nbursts > 1)
+            hipLaunchKernelGGL((rx_kernel<48, kDescStride, true, false>), dim3(g.blocks), dim3(256), 0, st, a);
+        else if (strided)
+            hipLaunchKernelGGL((rx_kernel<48, kDescStride, false, false>), dim3(g.blocks), dim3(256), 0, st, a);
+        else if (a.nbursts > 1)
             hipLaunchKernelGGL((rx_kernel<48, kDescList, true, false>), dim3(g.blocks), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((rx_kernel<48, kDescList, false, false>), dim3(g.blocks), dim3(256), 0, st, a);
@@ -209,6 +213,21 @@ hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets,
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(mirror_patch, dim3((n + 255u) / 256u), dim3(256), 0, st, p, n, buckets, listen, arp);
+    return hipGetLastError();
+}
+
+// A fixed-stride burst's offsets as a list (rxg_rx_bursts_strided_dev's bursts, for the
+// payload gather and the replay's re-classification, which read offsets through a list).
+__global__ __launch_bounds__(256) void strided_offsets(uint32_t *off, uint32_t n, uint32_t slot0, uint32_t stride64)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) off[i] = slot0 + i * stride64;
+}
+
+hipError_t launch_strided_offsets(uint32_t *off, uint32_t n, uint32_t slot0, uint32_t stride64, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(strided_offsets, dim3(std::min(1024u, (n + 255u) / 256u)), dim3(256), 0, st, off, n, slot0,
+                       stride64);
     return hipGetLastError();
 }
 

@@ -142,6 +142,11 @@ class DevBurst(C.Structure):
                 ("out", C.c_void_p)]
 
 
+class DevStridedBurst(C.Structure):
+    """rxg_dev_strided_burst: one burst of a fixed-stride launch (rxg_rx_bursts_strided_dev)."""
+    _fields_ = [("len", C.c_void_p), ("n", C.c_uint32), ("slot0", C.c_uint32), ("out", C.c_void_p)]
+
+
 class DevTxBatch(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("off64", C.c_void_p), ("len", C.c_void_p),
                 ("n", C.c_uint32), ("pad", C.c_uint32)]
@@ -240,6 +245,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_arp_disable": (C.c_int, [vp]),
         "rxg_rx_burst_dev": (C.c_int, [vp, C.POINTER(DevBatch), vp]),
         "rxg_rx_bursts_dev": (C.c_int, [vp, vp, vp, u32, u32, vp]),
+        "rxg_rx_bursts_strided_dev": (C.c_int, [vp, vp, u32, vp, u32, u32, vp]),
         "rxg_rx_burst": (C.c_int, [vp, C.POINTER(PktView), u32, u32, vp]),
         "rxg_tx_cksum_dev": (C.c_int, [vp, C.POINTER(DevTxBatch), vp]),
         "rxg_server_start": (C.c_int, [vp, C.POINTER(ServerConfig)]),
@@ -585,6 +591,13 @@ class Engine:
         arr = (DevBurst * max(len(bursts), 1))(*[DevBurst(o, l, n, 0, out) for o, l, n, out in bursts])
         _check(_lib.rxg_rx_bursts_dev(self.ctx, frames, arr, len(bursts), rec_kind, stream),
                "rxg_rx_bursts_dev")
+
+    def rx_bursts_strided_dev(self, frames: int, stride64: int, bursts, rec_kind: int = REC16, stream=None):
+        """bursts: [(slot0, len ptr, n, out ptr), ...]: frame i of a burst at 64-byte slot
+        slot0 + i * stride64 of the pool (no offset list), one launch."""
+        arr = (DevStridedBurst * max(len(bursts), 1))(*[DevStridedBurst(l, n, s0, out) for s0, l, n, out in bursts])
+        _check(_lib.rxg_rx_bursts_strided_dev(self.ctx, frames, stride64, arr, len(bursts), rec_kind, stream),
+               "rxg_rx_bursts_strided_dev")
 
     # --- latency mode (rxg_server_*): a persistent kernel serves small bursts
     def server_start(self, rec_kind: int = REC8, blocks: int = 1, max_frames: int = 4096,

@@ -372,6 +372,24 @@ typedef struct rxg_dev_burst {
 int rxg_rx_bursts_dev(rxg_ctx *ctx, const void *frames, const rxg_dev_burst *bursts, uint32_t k,
                       uint32_t rec_kind, void *stream);
 
+/* Fixed-stride bursts: frame i of a burst occupies bytes [frames + 64 * (slot0 + i * stride64),
+   + len[i]), with the readability rules of rxg_dev_batch.  For frame pools of fixed-size
+   elements filled in ring order -- a DPDK mempool's elements are fixed-size (MBUF_SIZE,
+   main.c:94-95), and a receive ring whose buffers are such elements posted in order, or this
+   library's own host-burst staging, places frame i at a fixed stride -- the kernel then reads
+   no per-frame offset list: 4 bytes less per frame of descriptor traffic (of 14 per 64-byte
+   frame with 8-byte records).  Same records, counters, replay and payload gather as
+   rxg_rx_bursts_dev with off64[i] = slot0 + i * stride64 (slot0 + (n-1) * stride64 must fit
+   32 bits, else -EINVAL).  Asynchronous on `stream`. */
+typedef struct rxg_dev_strided_burst {
+    const uint16_t *len;    /* dev, n entries */
+    uint32_t n;
+    uint32_t slot0;         /* 64-byte slot of the burst's frame 0 in the pool */
+    void *out;              /* dev, n records */
+} rxg_dev_strided_burst;
+int rxg_rx_bursts_strided_dev(rxg_ctx *ctx, const void *frames, uint32_t stride64,
+                              const rxg_dev_strided_burst *bursts, uint32_t k, uint32_t rec_kind, void *stream);
+
 /* DPDK-compatible host packet view: frame = (char*)buf_addr + data_off, data_len bytes
    (struct rte_mbuf fields of the same names). */
 typedef struct rxg_pkt_view {

@@ -19,7 +19,7 @@ WL = {"c3": (1500, 1000, 0, 2), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3)}
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c3", choices=sorted(WL) + ["c2multi", "tx3", "tx4", "pg3", "pg4"])
+    ap.add_argument("--workload", default="c3", choices=sorted(WL) + ["c2s", "c2multi", "c2multis", "tx3", "tx4", "pg3", "pg4"])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rec", type=int, default=16, choices=[8, 16, 48])
@@ -27,11 +27,17 @@ def main():
     rec = args.rec
     eng = rxg.Engine(0)
     n = args.frames
-    if args.workload == "c2multi":  # bench.py multiburst_leg: 16 bursts of one 1 GiB pool per launch
+    if args.workload in ("c2multi", "c2multis"):  # bench.py multiburst_leg: 16 bursts of one 1 GiB pool per launch
         k = 16
         pool = eng.synth(n=n * k, nflows=1, len_a=64, mix=0, seed=0x5EED0001 + 123)
         eng.tcb_load(*rxg.synthetic_tcb_table(1))
         out = eng.alloc(n * k * rec)
+        if args.workload == "c2multis":  # the fixed-stride form: frame i of burst j at slot j n + i
+            sb = [(j * n, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * rec) for j in range(k)]
+            for _ in range(args.iters):
+                eng.rx_bursts_strided_dev(pool["arena"].ptr, 1, sb, rec)
+            eng.sync()
+            return
         bursts = [(pool["off64"].ptr + j * n * 4, pool["len"].ptr + j * n * 2, n, out.ptr + j * n * rec)
                   for j in range(k)]
         for _ in range(args.iters):
@@ -61,13 +67,17 @@ def main():
         eng.sync()
         assert int(used.download(np.uint64, 1)[0]) == cap
         return
-    L, flows, mix, copies = WL[args.workload]
+    strided = args.workload == "c2s"  # C2 through rxg_rx_bursts_strided_dev (frame i at slot i)
+    L, flows, mix, copies = WL["c2" if strided else args.workload]
     bs = [eng.synth(n=n, nflows=flows, len_a=L or 1500, mix=mix, seed=0x5EED0001 + 17 * c) for c in range(copies)]
     eng.tcb_load(*rxg.synthetic_tcb_table(flows))
     out = eng.alloc(n * rec)
     for i in range(args.iters):
         b = bs[i % copies]
-        eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, out.ptr, rec)
+        if strided:
+            eng.rx_bursts_strided_dev(b["arena"].ptr, 1, [(0, b["len"].ptr, n, out.ptr)], rec)
+        else:
+            eng.rx_burst_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, out.ptr, rec)
     eng.sync()
 
 

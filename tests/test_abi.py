@@ -186,10 +186,10 @@ def _kernel_instantiations(path):
 
 # The product kernels: round 3's set (every record kind single / multi-burst, the two-deep
 # REC8 / REC16 forms, tx, the REC16 re-classification through a selection list) plus the
-# fixed-stride REC8 / REC16 forms (DESC 2).
-PRODUCT_KERNELS = ({(m, 0, mu, dp, 0) for m in (8, 16) for mu in (0, 1) for dp in (0, 1)}
-                   | {(m, 2, mu, dp, 0) for m in (8, 16) for mu in (0, 1) for dp in (0, 1)}
-                   | {(48, 0, 0, 0, 0), (48, 0, 1, 0, 0), (0, 0, 0, 0, 0), (16, 1, 0, 0, 0)})
+# fixed-stride forms (DESC 2, rxg_rx_bursts_strided_dev).
+PRODUCT_KERNELS = ({(m, d, mu, dp, 0) for m in (8, 16) for d in (0, 2) for mu in (0, 1) for dp in (0, 1)}
+                   | {(48, d, mu, 0, 0) for d in (0, 2) for mu in (0, 1)}
+                   | {(0, 0, 0, 0, 0), (16, 1, 0, 0, 0)})
 
 
 def test_product_library_has_no_experiment_switches():

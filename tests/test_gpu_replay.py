@@ -126,14 +126,18 @@ def sequential_reference(rows, frames, verify=False, globals_out=None):
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_replay_sequential_equivalence(replay_engine, seed):
-    engine = replay_engine
+    run_replay_equivalence(replay_engine, seed)
+
+
+def run_replay_equivalence(engine, seed, burst=None):
+    """burst(engine, frames) -> REC16 records: the burst form under test (default rxg_rx_burst)."""
     rows, frames = scenario(seed)
     exp, ecnt, erows = sequential_reference(rows, frames)
     tcb, live = pktgen.table_arrays(rows)
     engine.tcb_load(tcb, live)
     engine.tcb_sync()
     engine.counters_reset()
-    recs = engine.rx_burst(frames, rxg.REC16)
+    recs = burst(engine, frames) if burst else engine.rx_burst(frames, rxg.REC16)
     model = Model(rows, engine)
     bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
     addr = {C.addressof(b): i for i, b in enumerate(bufs)}

@@ -207,7 +207,7 @@ def test_server_replay_sequential_equivalence(seed, on_device, flags):
                      flags=rxg.CFG_REPLAY_ON_DEVICE if on_device else 0)
     eng.server_start(rxg.REC16, blocks=2, max_frames=4096, flags=flags)
     try:
-        test_gpu_replay.test_replay_sequential_equivalence(eng, seed)
+        test_gpu_replay.run_replay_equivalence(eng, seed)
     finally:
         eng.close()
 
@@ -237,3 +237,108 @@ def test_launched_bursts_beside_a_running_server(srv_engine):
         eng.server_stop()
         for d in (d_arena, d_off, d_len, out):
             d.free()
+
+
+def _free_all(*objs):
+    for o in objs:
+        if isinstance(o, dict):
+            for v in o.values():
+                if isinstance(v, rxg.DevArray):
+                    v.free()
+        elif o is not None:
+            o.free()
+
+
+def test_server_alternating_participants():
+    """64 workgroups serve 2 100 requests whose sizes alternate so that the
+    number of participating workgroups P changes every request (32 frames: P = 1, 300: 2,
+    4 096: 16, 16 384: 64), so workgroups keep sitting requests out while others run the next
+    one.  Every served request's records equal the launched burst's of the same frames, and
+    the counters of the whole sequence equal those of the same sequence launched.  (Round 3's
+    forwarding let a workgroup that sat out read the next request's words under the old
+    request's number.)"""
+    eng = rxg.Engine(device=0)
+    n = 16384
+    dev = eng.synth(n=n, nflows=4096, mix=1, seed=404)
+    tcb, live = rxg.synthetic_tcb_table(4096)
+    eng.tcb_load(tcb, live)
+    ref, out = eng.alloc(n * 8), eng.alloc(n * 8)
+    rng = np.random.default_rng(404)
+    sizes = [32, 300, 4096, 16384]
+    reqs = []
+    for j in range(2100):
+        k = sizes[j % 4] if j % 7 else sizes[int(rng.integers(0, 4))]
+        i = int(rng.integers(0, n - k + 1))
+        reqs.append((i, k))
+    try:
+        eng.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, ref.ptr, rxg.REC8)
+        eng.sync()
+        exp = ref.download(np.uint8, n * 8)
+        # the counters of the sequence, launched
+        eng.counters_reset()
+        for i, k in reqs:
+            eng.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr + 4 * i, dev["len"].ptr + 2 * i, k, out.ptr, rxg.REC8)
+        eng.sync()
+        exp_cnt = eng.counters()
+        eng.server_start(rxg.REC8, blocks=64, max_frames=n)
+        eng.counters_reset()
+        for j, (i, k) in enumerate(reqs):
+            eng.server_burst_dev(dev["arena"].ptr, dev["off64"].ptr + 4 * i, dev["len"].ptr + 2 * i, k,
+                                 out.ptr + 8 * i, rxg.REC8)
+            if j % 5 == 0 or k == n:  # (every request's records at the end of the loop too)
+                got = out.download(np.uint8, k * 8, offset_bytes=8 * i)
+                assert got.tobytes() == exp[8 * i: 8 * (i + k)].tobytes(), (j, i, k)
+        assert eng.counters().tolist() == exp_cnt.tolist()
+        eng.server_stop()
+    finally:
+        _free_all(dev, ref, out)
+        eng.close()
+
+
+@pytest.mark.parametrize("flags", [0, rxg.SRV_HOST_STAGING])
+def test_server_overflow_walks_see_mirror_writes(flags):
+    """the overflow walks (tuples and ARP addresses past their first bucket)
+    of the resident server read the mirror as it stands after writes made between requests.
+    64 K TCBs at the mirror's load (full first buckets are common: ~0.4 % of the probes walk),
+    a thousand removals / re-insertions between served bursts (backward-shift deletions move
+    tuples across buckets) and ARP addresses learned between them: every served burst equals
+    the same burst launched on the same table."""
+    eng = rxg.Engine(device=0)
+    nflows, n = 65536, 8192
+    dev = eng.synth(n=n, nflows=nflows, len_a=64, seed=505, with_flows=True)
+    tcb, live = rxg.synthetic_tcb_table(nflows)
+    live = live.copy()
+    eng.tcb_load(tcb, live)
+    srcs = tcb["ipv4_src"][1:]
+    eng.arp_load(srcs[: nflows // 2])
+    learned = nflows // 2
+    ref, out = eng.alloc(n * 16), eng.alloc(n * 16)
+    rng = np.random.default_rng(505)
+    try:
+        eng.server_start(rxg.REC16, blocks=8, max_frames=n, flags=flags)
+        for step in range(12):
+            for idx in rng.choice(np.arange(1, nflows + 1), size=1000, replace=False):
+                idx = int(idx)
+                if live[idx]:
+                    live[idx] = 0
+                    eng.tcb_remove(idx)
+                else:
+                    live[idx] = 1
+                    t = tcb[idx]
+                    eng.tcb_upsert(idx, int(t["dport"]), int(t["sport"]), int(t["ipv4_dst"]), int(t["ipv4_src"]),
+                                   int(t["state"]), int(t["identifier"]))
+            for ip in srcs[learned: learned + 1500]:
+                eng.arp_learned(int(ip))
+            learned += 1500
+            eng.server_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out.ptr, rxg.REC16)
+            got = out.download(np.uint8, n * 16)
+            eng.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, ref.ptr, rxg.REC16)
+            eng.sync()
+            exp = ref.download(np.uint8, n * 16)
+            assert got.tobytes() == exp.tobytes(), step
+            r = got.view(rxg.REC16_DTYPE)
+            assert (r["flags"] & rxg.F_ARP_LEARN).any() and not (r["flags"] & rxg.F_ARP_LEARN).all()
+        eng.server_stop()
+    finally:
+        _free_all(dev, ref, out)
+        eng.close()
