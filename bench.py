@@ -747,10 +747,10 @@ def main():
         eng.tcb_load(tcb, live)
 
     # The reference rx path is one lcore (main.c:366-369): its baseline is a host figure,
-    # independent of N.  Rank 0 times it after the timed region at any N; the other ranks
-    # wait at the barrier.
+    # independent of N, timed by rank 0 after the timed region of the N = 1 run only (the
+    # driver's N > 1 lines carry null; the other ranks would only wait at the barrier).
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
         cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds, cores=cores)
     barrier(device)

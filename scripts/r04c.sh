@@ -12,3 +12,5 @@ for k,v in d['legs'].items():
 "
 timeout -k 10 400 python3 scripts/kbench.py --variants 0:0,63:0,61:0,60:0,62:0,13:0 --workloads c4,u64 --rec 8 --rounds 5 > gpurun_out/r04c/c4_decomp.jsonl 2> gpurun_out/r04c/c4_decomp.err || { tail -5 gpurun_out/r04c/c4_decomp.err; exit 1; }
 cat gpurun_out/r04c/c4_decomp.jsonl
+timeout -k 10 120 ./dpdk-tcpipstack_amd/build/txscatter > gpurun_out/r04c/txscatter.jsonl 2>&1 || exit 1
+cat gpurun_out/r04c/txscatter.jsonl
