@@ -38,10 +38,10 @@ TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.jso
                  ("c2_64B_1flow", 1 << 20, 16): "profiles/r02/c2/traffic.json",
                  ("c4_imix_64Kflows", 1 << 20, 16): "profiles/r02/c4/traffic.json",
                  ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r02/c2multi/traffic.json",
-                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r03/final/c3/traffic.json",
-                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r03/final/c2/traffic.json",
-                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r03/final/c4/traffic.json",
-                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r03/final/c2multi/traffic.json",
+                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r04/c3/traffic.json",
+                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r04/c2/traffic.json",
+                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r04/c4/traffic.json",
+                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r04/c2multi/traffic.json",
                  # the 8(f) kernels over the headline's C3 batch (scripts/gpu_prof.sh tx3 / pg3)
                  ("tx_generate_dev", 1 << 20, 8): "profiles/r03/final/tx3/traffic.json",
                  ("payload_gather", 1 << 20, 8): "profiles/r03/final/pg3/traffic.json",
