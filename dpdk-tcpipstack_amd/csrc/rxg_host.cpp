@@ -1240,9 +1240,14 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
     L.max_blocks = c->max_blocks ? c->max_blocks : c->grid_tx;
     if (L.max_blocks == 0) L.max_blocks = 1024;
 #ifdef RXG_EXPERIMENTS
-    if (c->variant == 90) {
+    L.variant = c->variant;
+    if (c->variant == 90 || c->variant == 92) {
         if ((rc = ensure(c->d_exp_ck, (size_t)b->n * 4u))) return rc;
         HIP_OK(launch_tx_two_pass_exp(L, (uint32_t *)c->d_exp_ck.p, pick(c, stream)));
+        return 0;
+    }
+    if (c->variant == 91) {
+        HIP_OK(launch_tx_exp(L, pick(c, stream)));
         return 0;
     }
 #endif

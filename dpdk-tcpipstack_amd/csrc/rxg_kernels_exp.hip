@@ -13,6 +13,8 @@
 // RXG_VARIANT (rxg_tx_cksum_dev):
 //   90      two passes: the checksums of every frame into an array (rx_kernel<kModeTxWords>, no
 //           store into the frames), then tx_scatter writes the two fields of each frame; exact
+//   91      the production tx kernel with its rounds not software-pipelined; exact
+//   92      90 with pass 1's rounds not pipelined; exact
 // RXG_VARIANT (latency-mode server, record kind 8):
 //   79 / 80 / 81 / 82  the server without its rx body / its request acquire / its release
 //                      before `done` / both of the last two (SRVX 1 / 2 / 4 / 6)
@@ -72,6 +74,17 @@ __global__ __launch_bounds__(256) void tx_scatter(uint8_t *frames, const uint32_
     }
 }
 
+hipError_t launch_tx_exp(const LaunchRx &L, hipStream_t st)
+{
+    RxArgs a;
+    RxGrid g;
+    const hipError_t e = rx_args(L, a, g);
+    if (e != hipSuccess || a.nslices == 0) return e;
+    if (L.variant != 91 || a.nbursts != 1 || L.stride64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((rx_kernel<0, kDescList, false, false, kFormNoPipe>), dim3(g.blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_tx_two_pass_exp(const LaunchRx &L, uint32_t *ck, hipStream_t st)
 {
     if (L.nbursts != 1 || L.sel || L.stride64) return hipErrorInvalidValue;
@@ -83,7 +96,11 @@ hipError_t launch_tx_two_pass_exp(const LaunchRx &L, uint32_t *ck, hipStream_t s
     RxGrid g;
     hipError_t e = rx_args(X, a, g);
     if (e != hipSuccess || a.nslices == 0) return e;
-    hipLaunchKernelGGL((rx_kernel<kModeTxWords, kDescList, false, false>), dim3(g.blocks), dim3(256), 0, st, a);
+    if (L.variant == 92)
+        hipLaunchKernelGGL((rx_kernel<kModeTxWords, kDescList, false, false, kFormNoPipe>), dim3(g.blocks), dim3(256), 0,
+                           st, a);
+    else
+        hipLaunchKernelGGL((rx_kernel<kModeTxWords, kDescList, false, false>), dim3(g.blocks), dim3(256), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t n = b.n;
     hipLaunchKernelGGL(tx_scatter, dim3(std::min(4096u, (n + 255u) / 256u)), dim3(256), 0, st,

@@ -836,6 +836,7 @@ constexpr int kAblNoStore = 2;      // no record stores
 constexpr int kAblNoPhaseB = 4;     // no classify at all (parse + checksums only)
 constexpr int kAblHotBuckets = 8;   // every probe reads one of the first 256 buckets (cache-resident)
 constexpr int kAblNoSearch = 16;    // the first bucket's first slot taken as the hit: loads without the search
+constexpr int kFormNoPipe = 32;     // (a form, exact) tx / server rounds not software-pipelined
 // First bucket of the exact-tuple probe, loaded early so that several frames' probes of
 // one lane are in flight together.
 struct Probe {
@@ -1608,7 +1609,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         // VGPRs) and in the server; in launched rx, at the occupancy grid, the second buffer's
         // register cap cost more than the overlap gained.  Multi-burst kernels keep the plain
         // form: with the burst table held in lanes the pipelined rounds need 176 VGPRs.
-        constexpr bool PIPE = !MULTI && (MODE < 8 || SRV);
+        constexpr bool PIPE = !MULTI && (MODE < 8 || SRV) && !(ABL & kFormNoPipe);
         // classes 0-2 of mixed slices: plain loads; the larger ones non-temporal (measured
         // +5 % at 1500 B, -4 % at 64 B)
         run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
