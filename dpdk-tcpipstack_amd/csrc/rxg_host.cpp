@@ -1241,7 +1241,7 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
     if (L.max_blocks == 0) L.max_blocks = 1024;
 #ifdef RXG_EXPERIMENTS
     L.variant = c->variant;
-    if (c->variant == 90 || c->variant == 92) {
+    if (c->variant == 90 || c->variant == 92 || c->variant == 93) {
         if ((rc = ensure(c->d_exp_ck, (size_t)b->n * 4u))) return rc;
         HIP_OK(launch_tx_two_pass_exp(L, (uint32_t *)c->d_exp_ck.p, pick(c, stream)));
         return 0;

@@ -15,6 +15,7 @@
 //           store into the frames), then tx_scatter writes the two fields of each frame; exact
 //   91      the production tx kernel with its rounds not software-pipelined; exact
 //   92      90 with pass 1's rounds not pipelined; exact
+//   93      pass 1 of 90 alone (timing only: no checksum reaches the frames)
 // RXG_VARIANT (latency-mode server, record kind 8):
 //   79 / 80 / 81 / 82  the server without its rx body / its request acquire / its release
 //                      before `done` / both of the last two (SRVX 1 / 2 / 4 / 6)
@@ -102,6 +103,7 @@ hipError_t launch_tx_two_pass_exp(const LaunchRx &L, uint32_t *ck, hipStream_t s
     else
         hipLaunchKernelGGL((rx_kernel<kModeTxWords, kDescList, false, false>), dim3(g.blocks), dim3(256), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (L.variant == 93) return hipSuccess;
     const uint32_t n = b.n;
     hipLaunchKernelGGL(tx_scatter, dim3(std::min(4096u, (n + 255u) / 256u)), dim3(256), 0, st,
                        const_cast<uint8_t *>(L.frames), b.off64, b.len, ck, n);

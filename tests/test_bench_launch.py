@@ -7,6 +7,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -23,15 +25,16 @@ def _lines(out):
     return [json.loads(s) for s in out.splitlines() if s.startswith("{")]
 
 
-def test_gpus_2_spawns_two_ranks():
-    r = _run(["--gpus", "2", "--no-legs", "--no-cpu"], {"RXG_BENCH_REHEARSE": "1"})
+@pytest.mark.parametrize("n", [2, 4])
+def test_gpus_n_spawns_n_ranks(n):
+    r = _run(["--gpus", str(n), "--no-legs", "--no-cpu"], {"RXG_BENCH_REHEARSE": "1"})
     assert r.returncode == 0, r.stderr[-2000:]
     lines = _lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
     line = lines[0]
-    assert line["n_gpus"] == 2 and line["ranks"] == 2
-    assert sorted(d["rank"] for d in line["devices"]) == [0, 1]
-    assert line["max_over_ranks_check"] == 2.0  # the gloo all-reduce saw both ranks
+    assert line["n_gpus"] == n and line["ranks"] == n
+    assert sorted(d["rank"] for d in line["devices"]) == list(range(n))
+    assert line["max_over_ranks_check"] == float(n)  # the gloo all-reduce saw every rank
 
 
 def test_gpus_1_is_one_process():
