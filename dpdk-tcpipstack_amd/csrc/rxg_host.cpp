@@ -168,9 +168,6 @@ struct rxg_ctx {
     const uint32_t *last_off = nullptr;  // nullptr: a fixed-stride burst (burst_offsets)
     uint32_t last_slot0 = 0, last_stride64 = 0;
     DevBuf d_soff;                       // a fixed-stride burst's offsets, written on demand
-#ifdef RXG_EXPERIMENTS
-    DevBuf d_exp_ck;                     // RXG_VARIANT 90: the two-pass tx's checksum words
-#endif
     uint32_t soff_slot0 = 0, soff_stride64 = 0, soff_n = 0;  // what d_soff holds (n 0: nothing),
     hipStream_t soff_stream = nullptr;                        // written on this stream
     const uint16_t *last_len = nullptr;
@@ -376,9 +373,6 @@ extern "C" int rxg_fini(rxg_ctx *c)
     for (DevBuf *b : {&c->buckets, &c->listen, &c->d_sel, &c->d_fix, &c->d_arp, &c->d_pg_status, &c->d_pg_ticket,
                       &c->d_soff})
         if (b->p) (void)hipFree(b->p);
-#ifdef RXG_EXPERIMENTS
-    if (c->d_exp_ck.p) (void)hipFree(c->d_exp_ck.p);
-#endif
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
     for (auto &pb : c->patch) {
@@ -1239,18 +1233,6 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
     L.counters = nullptr;
     L.max_blocks = c->max_blocks ? c->max_blocks : c->grid_tx;
     if (L.max_blocks == 0) L.max_blocks = 1024;
-#ifdef RXG_EXPERIMENTS
-    L.variant = c->variant;
-    if (c->variant == 90 || c->variant == 92 || c->variant == 93) {
-        if ((rc = ensure(c->d_exp_ck, (size_t)b->n * 4u))) return rc;
-        HIP_OK(launch_tx_two_pass_exp(L, (uint32_t *)c->d_exp_ck.p, pick(c, stream)));
-        return 0;
-    }
-    if (c->variant == 91) {
-        HIP_OK(launch_tx_exp(L, pick(c, stream)));
-        return 0;
-    }
-#endif
     HIP_OK(launch_rx(L, pick(c, stream)));
     return 0;
 }

@@ -140,9 +140,6 @@ struct LaunchServer {
 hipError_t launch_server(const LaunchServer &L, hipStream_t st);
 #ifdef RXG_EXPERIMENTS
 hipError_t launch_server_exp(const LaunchServer &L, hipStream_t st);  // rxg_kernels_exp.hip
-// two-pass tx (RXG_VARIANT 90): checksums into ck[n], then written into the frames
-hipError_t launch_tx_two_pass_exp(const LaunchRx &L, uint32_t *ck, hipStream_t st);
-hipError_t launch_tx_exp(const LaunchRx &L, hipStream_t st);  // RXG_VARIANT 91
 #endif
 // rxg_payload.hip: gather of the burst's candidate payloads (one launch + a memset)
 hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *tickets_used);

@@ -204,11 +204,6 @@ struct Rec {
 // frame's ORIGINAL lane (its descriptor lane) for phase B.  MODE 0: transmit checksum
 // generate, written straight into the frame.
 //
-// MODE kModeTxWords: tx checksum generate whose checksums go to an array (4 bytes per frame,
-// {ip_ck, tcp_ck} as computed, the fields zeroed while summing) instead of into the frames;
-// a second pass writes them in (two-pass tx, experiment library).
-constexpr int kModeTxWords = 4;
-
 // LDS field rows (per wave, [field][64 lanes]):
 enum { F_CK = 0, F_ET, F_PORTS, F_SRC, F_DST, F_TL, F_SEQ, F_ACK, F_H1, F_H2, NF16 = 6, NF48 = 10 };
 
@@ -227,7 +222,6 @@ template <int MODE>
 __device__ __forceinline__ void park_fields(uint32_t *sf, uint32_t orig, const Fields &F)
 {
     sf[F_CK * 64 + orig] = F.ck;
-    if constexpr (MODE == kModeTxWords) return;  // two-pass tx: the checksums alone
     sf[F_ET * 64 + orig] = F.et;
     sf[F_PORTS * 64 + orig] = F.ports;
     sf[F_SRC * 64 + orig] = F.src;
@@ -298,7 +292,7 @@ template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
 __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                int lane, uint32_t (&d)[NLOAD][4])
 {
-    constexpr bool TX = MODE == 0 || MODE == kModeTxWords;
+    constexpr bool TX = MODE == 0;
     const int gl = lane & (LPF - 1);
     const int gbase = lane - gl;
     const bool leader = active && gl == 0;
@@ -398,7 +392,7 @@ __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, ui
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
-    if constexpr (MODE == 0) {
+    if constexpr (TX) {
         // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118); bytes at or
         // beyond data_len are never written
         if (leader) {
@@ -500,7 +494,7 @@ __device__ __forceinline__ void full_sum(const uint32_t (&q)[4], uint32_t w, uin
 template <int MODE>
 __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32_t (&q)[4][4])
 {
-    constexpr bool TX = MODE == 0 || MODE == kModeTxWords;
+    constexpr bool TX = MODE == 0;
     uint32_t h1 = q[0][1], h2 = q[0][2], h3 = q[0][3], h4 = q[1][0], h5 = q[1][1], h6 = q[1][2];
     uint32_t h7 = q[1][3], h8 = q[2][0], h9 = q[2][1], h10 = q[2][2], h11 = q[2][3];
     if (__ballot(len < 54u) != 0ull) {  // bytes at/after data_len read as zero (rare)
@@ -544,7 +538,7 @@ __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
-    if constexpr (MODE == 0) {
+    if constexpr (TX) {
         // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118); bytes at or
         // beyond data_len are never written.  Two 2-byte stores: rewriting a 64-byte frame's
         // whole line instead measured slower, C4 tx 101.4 against 94.5 us, 64 B frames 40.9
@@ -600,7 +594,7 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
                                                       int lane, uint32_t (&d)[NLOAD][4])
 {
     static_assert(LPF >= 2 && LPF <= 64, "streaming classes only");
-    constexpr bool TX = MODE == 0 || MODE == kModeTxWords;
+    constexpr bool TX = MODE == 0;
     const int gl = lane & (LPF - 1);
     const int gbase = lane - gl;
     const bool leader = active && gl == 0;
@@ -689,7 +683,7 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
-    if constexpr (MODE == 0) {
+    if constexpr (TX) {
         // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118).  Frames of
         // these classes are longer than 64 bytes: the group writes the frame's whole first
         // 64-byte line (chunks 0-3, as loaded, with the two checksum fields set) rather
@@ -836,7 +830,6 @@ constexpr int kAblNoStore = 2;      // no record stores
 constexpr int kAblNoPhaseB = 4;     // no classify at all (parse + checksums only)
 constexpr int kAblHotBuckets = 8;   // every probe reads one of the first 256 buckets (cache-resident)
 constexpr int kAblNoSearch = 16;    // the first bucket's first slot taken as the hit: loads without the search
-constexpr int kFormNoPipe = 32;     // (a form, exact) tx / server rounds not software-pipelined
 // First bucket of the exact-tuple probe, loaded early so that several frames' probes of
 // one lane are in flight together.
 struct Probe {
@@ -1519,10 +1512,8 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     // small-slice transpose, NF x 256 B parked fields), so LDS per wave is the ring alone.
     // 3 workgroups per CU (LDS and, at ~145 VGPRs, registers).
     // (tx, MODE 0: 4 x 1 KiB, the class-0 transpose's scratch; no records)
-    // (two-pass tx, MODE kModeTxWords: 6 x 1 KiB, the checksum row and the transpose)
-    constexpr bool TXW = MODE == kModeTxWords;
-    constexpr int RS = MODE == 16 ? 11 : MODE == 48 ? 4 : MODE == 8 ? 22 : TXW ? 6 : 4;
-    constexpr int kSlot = ring_slot_u4(MODE < 8 ? 16 : MODE);
+    constexpr int RS = MODE == 16 ? 11 : MODE == 48 ? 4 : MODE == 8 ? 22 : 4;
+    constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE);
     static_assert(MODE == 0 || (RS * kSlot * 16 >= 4096 + kSlot * 16 && RS * kSlot * 16 >= NF * 256 + 4096),
                   "ring too small for the scratch");
     __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kSlot];
@@ -1536,7 +1527,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
 #pragma unroll
     for (int k = 0; k < RXG_NCOUNTERS; ++k) wc.c[k] = 0u;
     unsigned long long bytes = 0ull;
-    RecRing<MODE < 8 ? 16 : MODE, RS> ring;
+    RecRing<MODE == 0 ? 16 : MODE, RS> ring;
     ring.img = s_rec[wid];
     ring.base = s_recf[wid];
     Rec rec;
@@ -1555,7 +1546,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         const bool valid = (uint32_t)lane < slice_frames(a, uniform(s), bc);
         const uint32_t off = c_off, len = valid ? c_len : 0u;
         const int cls = valid ? size_class(len) : 9;
-        if constexpr (MODE >= 8) {
+        if constexpr (MODE != 0) {
             if (__ballot(cls == 0) == ~0ull) {
                 // A run of all-small slices (every frame <= 64 bytes; lane i owns frame i end
                 // to end), prefetched one slice deep: the next slice's frame loads are issued
@@ -1604,12 +1595,12 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         uint32_t y_off = 0u, y_len = 0u;
         load_desc<DESC>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
         // parked fields, and the 4 KiB class-0 transpose after them
-        uint32_t *sf = MODE < 8 ? reinterpret_cast<uint32_t *>(ring.img[0]) : ring.scratch(a, lane, NF * 256 + 4096, bc);
+        uint32_t *sf = MODE == 0 ? reinterpret_cast<uint32_t *>(ring.img[0]) : ring.scratch(a, lane, NF * 256 + 4096, bc);
         // The streaming classes' rounds software-pipelined in tx (MODE 0, 101
         // VGPRs) and in the server; in launched rx, at the occupancy grid, the second buffer's
         // register cap cost more than the overlap gained.  Multi-burst kernels keep the plain
         // form: with the burst table held in lanes the pipelined rounds need 176 VGPRs.
-        constexpr bool PIPE = !MULTI && (MODE < 8 || SRV) && !(ABL & kFormNoPipe);
+        constexpr bool PIPE = !MULTI && (MODE == 0 || SRV);
         // classes 0-2 of mixed slices: plain loads; the larger ones non-temporal (measured
         // +5 % at 1500 B, -4 % at 64 B)
         run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
@@ -1622,18 +1613,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         run_class<5, 16, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
         run_class<6, 32, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
         run_class<7, 64, 2, true, MODE, true>(a, cls, off, len, lane, sf);
-        if constexpr (TXW) {
-            // the slice's checksum words, one coalesced 256-byte store
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t k = bc.of(a, s);
-            if (valid)
-                reinterpret_cast<uint32_t *>(bc.out_of(a, k))[(s - bc.slice0_of(a, k)) * 64u + (uint32_t)lane] =
-                    sf[F_CK * 64 + lane];
-            __builtin_amdgcn_wave_barrier();  // reads before the next slice's parking
-            wcount(wc, RXG_C_RX, valid);
-        } else if constexpr (MODE == 0 || (ABL & kAblNoPhaseB)) {
+        if constexpr (MODE == 0 || (ABL & kAblNoPhaseB)) {
             wcount(wc, RXG_C_RX, valid);
         } else {
             // the fields parked by other lanes of this wave must be visible to this lane
@@ -1651,7 +1631,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         c_off = n_off; c_len = n_len;
         n_off = y_off; n_len = y_len;
     }
-    if constexpr (MODE >= 8) ring.flush(a, lane, bc);
+    if constexpr (MODE != 0) ring.flush(a, lane, bc);
 
     if (a.counters == nullptr) return;
     // wave -> workgroup -> one atomic per counter
@@ -1663,7 +1643,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < RXG_NCOUNTERS; ++k) s_cnt[wid][k] = wc.c[k];
-        if (MODE >= 8) s_cnt[wid][RXG_C_BYTES] = bytes;
+        if (MODE != 0) s_cnt[wid][RXG_C_BYTES] = bytes;
     }
     __syncthreads();
     if (threadIdx.x < RXG_NCOUNTERS) {
