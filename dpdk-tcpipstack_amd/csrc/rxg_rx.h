@@ -115,6 +115,18 @@ struct RxArgs {
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
+// A device pointer rebuilt from an integer (readlane'd or read from LDS) as a pointer into the
+// global address space: the address-space inference then emits global_load / global_store.
+// Through a plain generic pointer the compiler emits flat loads and stores, which also count
+// in lgkmcnt, so every LDS wait after one waits for the HBM access too (the multi-burst
+// kernels' descriptor loads and record stores, and every access of the server's body).
+template <typename T>
+__device__ __forceinline__ T *as_global(uint64_t v)
+{
+    typedef __attribute__((address_space(1))) T gT;
+    return (T *)(gT *)v;
+}
+
 // The burst table of a multi-burst launch held in the wave's lanes: lane j keeps burst j's
 // slice0, n and pointers in VGPRs (loaded once per wave), so finding the burst of a slice is
 // one compare + ballot popcount and its fields are v_readlane -- no memory access and no
@@ -155,7 +167,7 @@ struct BurstCursor {
         const uint64_t v = (uint64_t)p;
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
         const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
-        return (T *)(((uint64_t)hi << 32) | lo);
+        return as_global<T>(((uint64_t)hi << 32) | lo);
     }
     __device__ __forceinline__ uint32_t slice0_of(const RxArgs &a, uint32_t k) const
     {
@@ -1817,22 +1829,22 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
             continue;
         }
         RxArgs a;
-        a.frames = reinterpret_cast<const uint8_t *>(uniform64((uint64_t)s_req.frames));
+        a.frames = as_global<const uint8_t>(uniform64((uint64_t)s_req.frames));
         a.sel = nullptr;
         a.nbursts = 1u;
         a.stride64 = 0u;
-        a.t.buckets = reinterpret_cast<const uint4 *>(uniform64((uint64_t)s_req.table.buckets));
-        a.t.listen = reinterpret_cast<const int32_t *>(uniform64((uint64_t)s_req.table.listen));
-        a.t.arp = reinterpret_cast<const uint4 *>(uniform64((uint64_t)s_req.table.arp));
+        a.t.buckets = as_global<const uint4>(uniform64((uint64_t)s_req.table.buckets));
+        a.t.listen = as_global<const int32_t>(uniform64((uint64_t)s_req.table.listen));
+        a.t.arp = as_global<const uint4>(uniform64((uint64_t)s_req.table.arp));
         a.t.bucket_mask = uniform(s_req.table.bucket_mask);
         a.t.ntcb = (int32_t)uniform((uint32_t)s_req.table.ntcb);
         a.t.min_null = (int32_t)uniform((uint32_t)s_req.table.min_null);
         a.t.arp_mask = uniform(s_req.table.arp_mask);
         a.t.arp_flags = uniform(s_req.table.arp_flags);
         a.counters = sa.counters;
-        a.b[0].off64 = reinterpret_cast<const uint32_t *>(uniform64((uint64_t)s_req.off64));
-        a.b[0].len = reinterpret_cast<const uint16_t *>(uniform64((uint64_t)s_req.len));
-        a.b[0].out = reinterpret_cast<uint8_t *>(uniform64((uint64_t)s_req.out));
+        a.b[0].off64 = as_global<const uint32_t>(uniform64((uint64_t)s_req.off64));
+        a.b[0].len = as_global<const uint16_t>(uniform64((uint64_t)s_req.len));
+        a.b[0].out = as_global<uint8_t>(uniform64((uint64_t)s_req.out));
         a.b[0].n = uniform(s_req.n);
         a.b[0].slice0 = 0u;
         a.nslices = (a.b[0].n + 63u) / 64u;
