@@ -115,11 +115,13 @@ struct RxArgs {
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-// A device pointer rebuilt from an integer (readlane'd or read from LDS) as a pointer into the
-// global address space: the address-space inference then emits global_load / global_store.
-// Through a plain generic pointer the compiler emits flat loads and stores, which also count
-// in lgkmcnt, so every LDS wait after one waits for the HBM access too (the multi-burst
-// kernels' descriptor loads and record stores, and every access of the server's body).
+// A device pointer rebuilt from an integer (read from LDS) as a pointer into the global
+// address space: the address-space inference then emits global_load / global_store.  Through a
+// plain generic pointer the compiler emits flat loads and stores, which also count in lgkmcnt,
+// so every LDS wait after one waits for the HBM access too.  Used for the server's request
+// (32 x 64 B served 9.1-9.3 us against 9.9 with flat accesses, profiles/r04/ab/r04m).  Not in
+// BurstCursor::rl_ptr: the multi-burst kernels measured slower with it (c2m 227.9 against
+// 217.0 us, same process), their waits being placed differently around the global accesses.
 template <typename T>
 __device__ __forceinline__ T *as_global(uint64_t v)
 {
@@ -167,7 +169,7 @@ struct BurstCursor {
         const uint64_t v = (uint64_t)p;
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
         const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
-        return as_global<T>(((uint64_t)hi << 32) | lo);
+        return (T *)(((uint64_t)hi << 32) | lo);
     }
     __device__ __forceinline__ uint32_t slice0_of(const RxArgs &a, uint32_t k) const
     {
