@@ -18,7 +18,8 @@ import sys
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("RXG_LIB") or os.path.join(_HERE, "librxg.so")
+_PRODUCT_LIB = os.path.join(_HERE, "librxg.so")
+LIB_PATH = os.environ.get("RXG_LIB") or _PRODUCT_LIB
 
 # ---------------------------------------------------------------- constants (rxg.h) ---
 ETHER_TYPE_IPV4 = 0x0800
@@ -306,8 +307,8 @@ def load_library(path: str = LIB_PATH):
         "rxg_group_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
-        if path != LIB_PATH and not hasattr(lib, name):
-            continue  # an older build loaded for an A/B (scripts/kbench.py): its own entry points only
+        if os.path.abspath(path) != _PRODUCT_LIB and not hasattr(lib, name):
+            continue  # another build loaded for an A/B (kbench.py, RXG_LIB): its own entry points only
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
