@@ -172,7 +172,7 @@ def time_workload(eng, wl, steps, warmup, device, stream, strided=False):
     return elapsed, kern_ms
 
 
-def time_region(eng, wl, steps, warmup, device, stream):
+def time_region(eng, wl, steps, warmup, device, stream, strided=False):
     """The headline's timed region: `steps` launches back to back on `stream`, one HIP event
     pair around all of them (recorded on that stream), nothing between them.  An event pair
     around every launch adds ~6 us of wall time per launch (scripts/evgap.cpp,
@@ -180,7 +180,7 @@ def time_region(eng, wl, steps, warmup, device, stream):
     per-launch distribution is taken in a separate pass (time_workload).  Returns the host
     wall seconds and the region's event milliseconds."""
     for i in range(warmup):
-        wl.launch(eng, i, stream)
+        wl.launch(eng, i, stream, strided)
     eng.sync()
     eng.counters_reset()
     e0, e1 = eng.event(), eng.event()
@@ -188,7 +188,7 @@ def time_region(eng, wl, steps, warmup, device, stream):
     t0 = time.perf_counter()
     eng.record(e0, stream)
     for i in range(steps):
-        wl.launch(eng, warmup + i, stream)
+        wl.launch(eng, warmup + i, stream, strided)
     eng.record(e1, stream)
     eng.sync()
     barrier(device)
@@ -204,7 +204,7 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=
     in one 1 GiB frame pool (the same working set as the rotating C2 leg, beyond the 256 MB
     Infinity Cache), classified by ONE launch (rxg_rx_bursts_dev) instead of one launch per
     burst: the launch ramp and drain are paid once per ring.  Roofline per launch =
-    nbursts x 64 MiB of frame bytes / the launch's event time."""
+    nbursts x 64 MiB of frame bytes / (the launches' event time / launches)."""
     pool = eng.synth(n=n * nbursts, nflows=1, len_a=64, mix=0, seed=seed + 123)
     tcb, live = rxg.synthetic_tcb_table(1)
     eng.tcb_load(tcb, live)
@@ -224,17 +224,19 @@ def multiburst_leg(eng, steps, warmup, device, seed, nbursts=16, n=1 << 20, rec=
             launch()
         eng.sync()
         eng.counters_reset()
-        evs = [(eng.event(), eng.event()) for _ in range(steps)]
+        e0, e1 = eng.event(), eng.event()
         barrier(device)
         t0 = time.perf_counter()
-        for a, b in evs:
-            eng.record(a)
+        eng.record(e0)  # one event pair around the launches (time_region)
+        for _ in range(steps):
             launch()
-            eng.record(b)
+        eng.record(e1)
         eng.sync()
         barrier(device)
         dt = max_over_ranks(time.perf_counter() - t0, device)
-        k = max_over_ranks(float(np.mean([eng.elapsed_ms(a, b) for a, b in evs])) / 1e3, device)
+        k = max_over_ranks(eng.elapsed_ms(e0, e1) / steps / 1e3, device)
+        eng.event_destroy(e0)
+        eng.event_destroy(e1)
         c = merge_counters(eng.counters(), device)
         frames_all = int(sum_over_ranks(n * nbursts, device)) * steps
         alg = n * nbursts * 64
@@ -728,8 +730,8 @@ def main():
         # headline timing so that both see the same clocks
         other = rxg.REC16 if args.rec == rxg.REC8 else rxg.REC8
         ow = Workload(eng, args.workload, frames, seed, other)
-        _, ko = time_workload(eng, ow, args.steps, args.warmup, device, stream)
-        ka = max_over_ranks(float(np.mean(ko)) / 1e3, device)
+        _, ro = time_region(eng, ow, args.steps, args.warmup, device, stream)
+        ka = max_over_ranks(ro / args.steps / 1e3, device)
         legs[f"{args.workload}_rec{other}"] = {"kernel_us": round(ka * 1e6, 2),
                                                "roofline_frac": round(ow.bytes_per_batch / ka / 1e9 / HBM_PEAK_GBS, 4)}
         ow.free()
@@ -740,16 +742,18 @@ def main():
             lw = Workload(eng, wname, frames, seed + 99, args.rec)
             t2, l2 = rxg.synthetic_tcb_table(lw.flows)
             eng.tcb_load(t2, l2)
-            e2, k2 = time_workload(eng, lw, args.steps, args.warmup, device, stream, strided)
+            e2, r2 = time_region(eng, lw, args.steps, args.warmup, device, stream, strided)
             e2 = max_over_ranks(e2, device)
             c2 = merge_counters(eng.counters(), device)
-            ka = float(np.mean(k2)) / 1e3
+            ka = r2 / args.steps / 1e3
+            _, k2 = time_workload(eng, lw, args.steps, 2, device, stream, strided)
             ln = int(sum_over_ranks(lw.n, device)) * args.steps
             lb = int(sum_over_ranks(lw.bytes_per_batch, device)) * args.steps
             legs[name] = {
                 "mpps": round(ln / e2 / 1e6, 2),
                 "gbs": round(lb / e2 / 1e9, 2),
                 "kernel_us": round(ka * 1e6, 2),
+                "kernel_us_per_launch_pairs_median": round(float(np.median(k2)) * 1e3, 2),
                 "roofline_frac": round(lw.bytes_per_batch / ka / 1e9 / HBM_PEAK_GBS, 4),
                 "working_set_GiB": round(lw.copies * (lw.batches[0]["arena_bytes"]) / 2**30, 3),
                 "counters_ok": bool(int(c2[0]) == ln
