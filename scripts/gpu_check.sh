@@ -6,6 +6,8 @@
 #   pytest      the whole -m gpu suite
 #   smoke       __graft_entry__.smoke()
 #   bench       the default bench line (bench.json)
+#   benchprof   rocprofv3 --kernel-trace --stats of the bench command itself (headline only:
+#               --no-legs --no-cpu), so its kernel average sits beside the line's kernel_us
 #   rehearse    bench.py --gpus 2 (bench.py spawns its 2 ranks itself) on the box's one GPU
 #               (gloo collectives; a rehearsal, never a scaling figure)
 #   prof        rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes per workload
@@ -39,6 +41,7 @@ for S in "$@"; do
     pytest)    step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke)     step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)     step bench 500 python -u bench.py; cp "$OUT/bench.log" "$OUT/bench.json" ;;
+    benchprof) step benchprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/benchprof" -o run --output-format csv -- python3 -u bench.py --no-legs --no-cpu ;;
     rehearse)  step rehearse2 600 env RXG_BENCH_REHEARSE=1 python3 -u bench.py --gpus 2 --steps 20 --warmup 3 ;;
     prof)      step prof 900 env REC=${REC:-8} bash scripts/gpu_prof.sh "$TAG/prof" ${PROF_WLS:-c3 c4 c2 c2multi} ;;
     sq)        step sq 600 env REC=${REC:-8} bash scripts/gpu_sq.sh ${SQ_WLS:-c4 c3} ;;
