@@ -226,6 +226,8 @@ struct rxg_ctx {
         bool on = false;        // configured (the kernel may have exited idle: relaunched on demand)
         rxg::SrvFsm<SrvPort> fsm;  // Down / Up / Failed (rxg_srvfsm.h)
         SrvReq req{};           // the request SrvPort::write posts
+        // its inline descriptors (kSrvInlineDesc): mailbox words 16-39, SrvMbox::ioff / ilen
+        alignas(16) unsigned long long idesc[kSrvPollWords - 16] = {};
         bool dev = false;       // arena / off / len in device memory (host writes only)
         bool mdev = false;      // mbox in device memory (large BAR, no RXG_SRV_HOST_MAILBOX)
         hipStream_t st = nullptr;
@@ -1042,21 +1044,25 @@ void SrvPort::write(unsigned long long q)
 {
     rxg_ctx::Server &S = c->srv;
     _mm_sfence();
-    const unsigned long long ck = srv_check(q, S.req);
+    const bool inl = (S.req.flags & kSrvInlineDesc) != 0u;
+    const unsigned long long ck = srv_check(q, S.req, inl ? S.idesc : nullptr);
     if (S.mdev) {
-        // Device mailbox (write-combined): the 128 bytes the server polls go out as two whole
-        // 64-byte lines (non-temporal 16-byte stores, one fence).
-        alignas(64) unsigned long long head[16] = {};
+        // Device mailbox (write-combined): the bytes the server polls go out as whole 64-byte
+        // lines (non-temporal 16-byte stores, one fence): 128, or 320 with inline descriptors.
+        alignas(64) unsigned long long head[kSrvPollWords] = {};
         static_assert(sizeof(SrvReq) + 8 <= offsetof(SrvMbox, check), "mailbox head layout");
         head[0] = q;
         std::memcpy(&head[1], &S.req, sizeof(SrvReq));
         head[offsetof(SrvMbox, check) / 8] = ck;
         head[offsetof(SrvMbox, stop) / 8] = 0ull;
+        if (inl) std::memcpy(&head[16], S.idesc, sizeof S.idesc);
         const __m128i *src = reinterpret_cast<const __m128i *>(head);
         __m128i *dst = reinterpret_cast<__m128i *>(S.mbox);
-        for (int i = 0; i < 8; ++i) _mm_stream_si128(dst + i, _mm_load_si128(src + i));
+        const int n16 = inl ? kSrvPollWords / 2 : 8;
+        for (int i = 0; i < n16; ++i) _mm_stream_si128(dst + i, _mm_load_si128(src + i));
         _mm_sfence();
     } else {
+        if (inl) std::memcpy(S.mbox->ioff, S.idesc, sizeof S.idesc);
         S.mbox->req = S.req;
         __atomic_store_n(&S.mbox->check, ck, __ATOMIC_RELEASE);
         __atomic_store_n(&S.mbox->seq, q, __ATOMIC_RELEASE);
@@ -1181,7 +1187,13 @@ extern "C" int rxg_server_placement(rxg_ctx *c)
     return c->srv.dev ? RXG_SRV_DEVICE : RXG_SRV_HOST;
 }
 
-extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b)
+// A served burst.  inl: a host burst of at most kSrvInline frames whose descriptors the
+// request carries in the mailbox (S.idesc, filled by the caller) as well as in the staging.
+static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl);
+
+extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b) { return server_burst(c, b, false); }
+
+static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl)
 {
     if (!c || !b) return fail(-EINVAL, "rxg_server_burst_dev: NULL argument");
     if (!c->srv.on) return fail(-ENODEV, "rxg_server_burst_dev: no server (rxg_server_start)");
@@ -1207,6 +1219,7 @@ extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b)
         r.len = b->len;
         r.out = (uint8_t *)b->out;
         r.n = b->n;
+        r.flags = inl && b->n <= kSrvInline ? kSrvInlineDesc : 0u;
         r.table = table_view(c);
         if ((rc = srv_post(c, r))) return rc;
     }
@@ -1261,8 +1274,17 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
                 if (pkts[i].data_len)
                     std::memcpy(S.arena + (uint64_t)S.h_off[i] * 64u,
                                 (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off, pkts[i].data_len);
+            // (the staged descriptors are also what a re-classification or a payload gather
+            // of this burst reads)
             std::memcpy(S.off, S.h_off.data(), (size_t)n * 4u);
             std::memcpy(S.len, S.h_len.data(), (size_t)n * 2u);
+            const bool inl = n <= kSrvInline;
+            if (inl) {
+                uint8_t *d = reinterpret_cast<uint8_t *>(S.idesc);
+                std::memset(d, 0, sizeof S.idesc);
+                std::memcpy(d, S.h_off.data(), (size_t)n * 4u);
+                std::memcpy(d + kSrvInline * 4u, S.h_len.data(), (size_t)n * 2u);
+            }
             rxg_dev_batch b;
             b.frames = S.arena;
             b.off64 = S.off;
@@ -1270,7 +1292,7 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
             b.n = n;
             b.rec_kind = rec_kind;
             b.out = S.out;
-            int rc = rxg_server_burst_dev(c, &b);
+            int rc = server_burst(c, &b, inl);
             if (rc) return rc;
             std::memcpy(out_host, S.out, (size_t)n * rec_kind);
             return 0;

@@ -77,32 +77,42 @@ struct SrvReq {
     const uint16_t *len;
     uint8_t *out;            // records of the server's kind
     uint32_t n;
-    uint32_t flags;          // reserved (0)
+    uint32_t flags;          // kSrvInlineDesc: the descriptors are in the mailbox (SrvMbox::ioff / ilen)
     DevTable table;          // the mirror as of the post
 };
-// Device memory written through the BAR (large-BAR GPUs, two whole lines per post) or coherent
+// Host bursts of up to kSrvInline frames carry their descriptors in the mailbox, on the lines
+// the server's poll reads with the request: its frame loads then wait for no descriptor load
+// (one dependent device-memory trip less per served burst).
+constexpr uint32_t kSrvInline = 32;
+constexpr uint32_t kSrvInlineDesc = 1u;
+// Device memory written through the BAR (large-BAR GPUs, whole lines per post) or coherent
 // host memory; `done` / `exited` are read from the server's return block (host memory, may
-// be a second SrvMbox).  The first 128 bytes are what the host writes and the server polls,
-// read whole by one wave instruction (16 lanes x 8 bytes): a request is taken when seq is new
-// and `check` is srv_check of seq and the request words.  Write-combined stores reach the
-// device as whole lines or in parts, in any order between lines until the host's fence: the
-// check word is what makes a snapshot holding words of two requests fail (it is then polled
-// again), not the order of the stores.  The server's words are on a line of their own.
+// be a second SrvMbox).  The first 320 bytes (words 0-39) are what the host writes and the
+// server polls, read whole by one wave instruction (40 lanes x 8 bytes): a request is taken
+// when seq is new and `check` is srv_check of seq, the request words and, for a request with
+// kSrvInlineDesc, the inline descriptor words 16-39.  Write-combined stores reach the device
+// as whole lines or in parts, in any order between lines until the host's fence: the check
+// word is what makes a snapshot holding words of two requests fail (it is then polled again),
+// not the order of the stores.  The server's words are on a line of their own.
 struct alignas(128) SrvMbox {
     unsigned long long seq;       // host: number of the request posted
     SrvReq req;
-    unsigned long long check;     // host: srv_check(seq, req)
+    unsigned long long check;     // host: srv_check(seq, req, ioff, ilen)
     unsigned long long stop;      // host: nonzero = exit
-    unsigned long long hpad[1];
+    unsigned long long hpad[2];
+    uint32_t ioff[kSrvInline];    // words 16-31: off64 of an inline request's frames
+    uint16_t ilen[kSrvInline];    // words 32-39: their lengths
     alignas(128) unsigned long long done;  // server: number of the last request finished
     unsigned long long exited;    // server: nonzero once the kernel has left its loop
 };
+constexpr int kSrvPollWords = 40;  // words 0-39: the request and its inline descriptors
 static_assert(sizeof(SrvReq) == 88, "mailbox layout");
-static_assert(offsetof(SrvMbox, check) == 96 && offsetof(SrvMbox, stop) == 104 && offsetof(SrvMbox, done) == 128,
+static_assert(offsetof(SrvMbox, check) == 96 && offsetof(SrvMbox, stop) == 104 && offsetof(SrvMbox, ioff) == 128 &&
+                  offsetof(SrvMbox, ilen) == 256 && offsetof(SrvMbox, done) == 384,
               "mailbox layout");
-// Word i (0 = seq, 1-11 = the request) of the mailbox mixed with its position; the check word
-// is the XOR of the twelve (a splitmix64 finaliser: any mix of old and new words changes it
-// but with probability 2^-64).
+// Word i of the mailbox (0 = seq, 1-11 = the request, 16-39 = inline descriptors) mixed with
+// its position; the check word is the XOR of the mixed words (a splitmix64 finaliser: any mix
+// of old and new words changes it but with probability 2^-64).
 __host__ __device__ inline unsigned long long srv_mix(unsigned i, unsigned long long w)
 {
     unsigned long long z = w + (unsigned long long)(i + 1u) * 0x9E3779B97F4A7C15ull;
@@ -110,12 +120,15 @@ __host__ __device__ inline unsigned long long srv_mix(unsigned i, unsigned long 
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-inline unsigned long long srv_check(unsigned long long seq, const SrvReq &r)
+// desc: words 16-39 of an inline request (nullptr otherwise)
+inline unsigned long long srv_check(unsigned long long seq, const SrvReq &r, const unsigned long long *desc)
 {
     unsigned long long w[sizeof(SrvReq) / 8];
     __builtin_memcpy(w, &r, sizeof w);
     unsigned long long h = srv_mix(0u, seq);
     for (unsigned i = 0; i < sizeof(SrvReq) / 8; ++i) h ^= srv_mix(i + 1u, w[i]);
+    if (desc)
+        for (unsigned i = 16; i < (unsigned)kSrvPollWords; ++i) h ^= srv_mix(i, desc[i - 16]);
     return h;
 }
 struct SrvCtl {                   // device memory

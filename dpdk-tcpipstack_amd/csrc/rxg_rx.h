@@ -1731,6 +1731,7 @@ template <int MODE, int SRVX = 0>
 __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
 {
     __shared__ SrvReq s_req;
+    __shared__ unsigned long long s_desc[kSrvPollWords - 16];  // an inline request's off64 / len
     __shared__ unsigned long long s_seq;  // the request's number (kSrvStop: exit)
     __shared__ uint32_t s_p;              // its participants
     // thread 0: the number of the last request seen.  It starts at `done` (the host sets go to
@@ -1740,15 +1741,16 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
     if (threadIdx.x == 0) last = __hip_atomic_load(&sa.ret->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
     for (;;) {
         if (blockIdx.x == 0 && threadIdx.x < 64) {
-            // wave 0 polls the mailbox's first 128 bytes (lane l < 16: bytes 8l .. 8l+7) in
-            // one instruction: the request arrives with its number, no second round trip
+            // wave 0 polls the mailbox's first 320 bytes (lane l < 40: bytes 8l .. 8l+7) in
+            // one instruction: the request arrives with its number and, for a small host
+            // burst, its descriptors (words 16-39): no second round trip before the frames
             const int l = (int)threadIdx.x;
             const unsigned long long lst = __shfl(last, 0, 64);
             const long long t0 = wall_clock64();
             unsigned long long q;
             for (;;) {
                 unsigned long long w = 0ull;
-                if (l < 16)
+                if (l < kSrvPollWords)
                     w = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(sa.mbox) + l, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_SYSTEM);
                 q = __shfl(w, 0, 64);
@@ -1758,13 +1760,25 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
                     break;
                 }
                 if (q != lst) {
-                    // the check word over the number and the request words (lanes 0-11): a
-                    // snapshot mixing two requests' words (a write-combined mailbox line
-                    // that reached the device in parts) fails it and is polled again
-                    const unsigned long long m = l < 12 ? srv_mix((unsigned)l, w) : 0ull;
+                    // the check word over the number, the request words (lanes 0-11) and an
+                    // inline request's descriptor words (lanes 16-39; SrvReq::flags is the
+                    // high half of word 5): a snapshot mixing two requests' words (a
+                    // write-combined mailbox line that reached the device in parts) fails it
+                    // and is polled again
+                    const bool inl = ((__shfl(w, 5, 64) >> 32) & kSrvInlineDesc) != 0ull;
+                    const bool mixed = l < 12 || (inl && l >= 16 && l < kSrvPollWords);
+                    const unsigned long long m = mixed ? srv_mix((unsigned)l, w) : 0ull;
                     const uint32_t lo = row_xor16((uint32_t)m), hi = row_xor16((uint32_t)(m >> 32));
-                    if ((((unsigned long long)hi << 32) | lo) == ck) {
+                    // the rows' XORs (lanes 48-63 hold none)
+                    const uint32_t xlo = (uint32_t)__builtin_amdgcn_readlane((int)lo, 0) ^
+                                         (uint32_t)__builtin_amdgcn_readlane((int)lo, 16) ^
+                                         (uint32_t)__builtin_amdgcn_readlane((int)lo, 32);
+                    const uint32_t xhi = (uint32_t)__builtin_amdgcn_readlane((int)hi, 0) ^
+                                         (uint32_t)__builtin_amdgcn_readlane((int)hi, 16) ^
+                                         (uint32_t)__builtin_amdgcn_readlane((int)hi, 32);
+                    if ((((unsigned long long)xhi << 32) | xlo) == ck) {
                         if (l >= 1 && l <= 11) reinterpret_cast<unsigned long long *>(&s_req)[l - 1] = w;  // bytes 8 .. 95
+                        if (inl && l >= 16 && l < kSrvPollWords) s_desc[l - 16] = w;
                         break;
                     }
                 }
@@ -1844,8 +1858,14 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
         a.t.arp_mask = uniform(s_req.table.arp_mask);
         a.t.arp_flags = uniform(s_req.table.arp_flags);
         a.counters = sa.counters;
-        a.b[0].off64 = as_global<const uint32_t>(uniform64((uint64_t)s_req.off64));
-        a.b[0].len = as_global<const uint16_t>(uniform64((uint64_t)s_req.len));
+        if (uniform(s_req.flags) & kSrvInlineDesc) {
+            // a small host burst: its descriptors came with the request (LDS, generic pointers)
+            a.b[0].off64 = reinterpret_cast<const uint32_t *>(s_desc);
+            a.b[0].len = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint8_t *>(s_desc) + kSrvInline * 4u);
+        } else {
+            a.b[0].off64 = reinterpret_cast<const uint32_t *>(uniform64((uint64_t)s_req.off64));
+            a.b[0].len = reinterpret_cast<const uint16_t *>(uniform64((uint64_t)s_req.len));
+        }
         a.b[0].out = as_global<uint8_t>(uniform64((uint64_t)s_req.out));
         a.b[0].n = uniform(s_req.n);
         a.b[0].slice0 = 0u;
