@@ -1017,7 +1017,7 @@ int SrvPort::launch()
     L.mode = (int)S.rec_kind;
 #ifdef RXG_EXPERIMENTS
     L.variant = c->variant;
-    if (c->variant >= 79 && c->variant <= 82) {
+    if (c->variant >= 79 && c->variant <= 89) {
         HIP_OK(launch_server_exp(L, S.st));
         return 0;
     }

@@ -13,6 +13,12 @@
 // RXG_VARIANT (latency-mode server, record kind 8):
 //   79 / 80 / 81 / 82  the server without its rx body / its request acquire / its release
 //                      before `done` / both of the last two (SRVX 1 / 2 / 4 / 6)
+//   83 / 84 / 85       the production server stamping each request's phases (SRVX 8,
+//                      scripts/srvstamps.py) / the same without the TCB probe / without the
+//                      record stores (SRVX 24 / 40)
+//   86 / 87            stamping, buckets from a cache-resident region / no search (SRVX 72 / 136)
+//   88                 stamping, the body's phases too (SRVX 264)
+//   89                 stamping, the body run twice per request (SRVX 520)
 #include <hip/hip_runtime.h>
 
 #include "rxg_kernels.h"
@@ -61,6 +67,13 @@ hipError_t launch_server_exp(const LaunchServer &L, hipStream_t st)
     case 80: hipLaunchKernelGGL((rx_server<8, 2>), g, b, 0, st, sa); break;
     case 81: hipLaunchKernelGGL((rx_server<8, 4>), g, b, 0, st, sa); break;
     case 82: hipLaunchKernelGGL((rx_server<8, 6>), g, b, 0, st, sa); break;
+    case 83: hipLaunchKernelGGL((rx_server<8, 8>), g, b, 0, st, sa); break;
+    case 84: hipLaunchKernelGGL((rx_server<8, 8 | 16>), g, b, 0, st, sa); break;
+    case 85: hipLaunchKernelGGL((rx_server<8, 8 | 32>), g, b, 0, st, sa); break;
+    case 86: hipLaunchKernelGGL((rx_server<8, 8 | 64>), g, b, 0, st, sa); break;
+    case 87: hipLaunchKernelGGL((rx_server<8, 8 | 128>), g, b, 0, st, sa); break;
+    case 88: hipLaunchKernelGGL((rx_server<8, 8 | 256>), g, b, 0, st, sa); break;
+    case 89: hipLaunchKernelGGL((rx_server<8, 8 | 512>), g, b, 0, st, sa); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -844,6 +844,17 @@ constexpr int kAblNoStore = 2;      // no record stores
 constexpr int kAblNoPhaseB = 4;     // no classify at all (parse + checksums only)
 constexpr int kAblHotBuckets = 8;   // every probe reads one of the first 256 buckets (cache-resident)
 constexpr int kAblNoSearch = 16;    // the first bucket's first slot taken as the hit: loads without the search
+constexpr int kAblStamps = 32;      // (server, one slice) lane 0 stamps the all-small step's phases
+                                    // into the words at RxArgs::sel (rx_server SRVX 256)
+template <int ABL>
+__device__ __forceinline__ void abl_stamp(const RxArgs &a, int lane, int k)
+{
+    if constexpr ((ABL & kAblStamps) != 0) {
+        const unsigned long long t = (unsigned long long)wall_clock64();
+        if (lane == 0 && (threadIdx.x >> 6) == 0)
+            reinterpret_cast<unsigned long long *>(const_cast<uint32_t *>(a.sel))[k] = t;
+    }
+}
 // First bucket of the exact-tuple probe, loaded early so that several frames' probes of
 // one lane are in flight together.
 struct Probe {
@@ -1427,9 +1438,14 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     // both in flight.  (Probe after the frames: the probe's wait drained the prefetch,
     // 64 B / 64 K flows 28.4 us.)
     const uint32_t s1 = s + nwaves;
+    // the server (VWALK) also runs a burst's last, partial slice here when its frames are all
+    // small (rx_body); a launch's runs are whole slices
+    const bool valid = !VWALK || (uint32_t)lane < slice_frames(a, uniform(s), bc);
     uint32_t d[4][4];
     uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
+    abl_stamp<ABL>(a, lane, 0);
     transpose_small_slice(vb[P], lane, sf, d);
+    abl_stamp<ABL>(a, lane, 1);
     // the next slice's descriptors are read after this slice's frames have landed: they were
     // issued before them (loop top) or just after (previous step), so this waits for no
     // more than the frames did
@@ -1442,6 +1458,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     // frames' LDS (as the class path does) measured 64 B at 64 K flows 28.8 -> 25.9 us, but
     // the one-flow C2 burst, which never probes, 19.2 -> 20.6 (more registers live across
     // the prefetch); the C2 configuration is the one the metric names.
+    abl_stamp<ABL>(a, lane, 2);
     const Probe PO = ((ABL & kAblNoProbe) || cached) ? probe_none() : probe_issue<ABL>(a, F);
     // The next slice's frames are issued whether or not the run continues (a run's last step
     // reads the arena's first bytes instead): the compiler cannot count a load issued under a
@@ -1450,12 +1467,15 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     issue_small_slice<true>(a, nxt ? n_off : 0u, nxt ? n_len : 0u, lane, vb[1 - P]);
     uint32_t y_off, y_len;
     load_desc<DESC>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
-    classify_finish<MODE, VWALK, ABL>(a, true, c_len, F, PO, wc, rec, fc, cached);
-    bytes += c_len;
+    abl_stamp<ABL>(a, lane, 3);
+    classify_finish<MODE, VWALK, ABL>(a, valid, c_len, F, PO, wc, rec, fc, cached);
+    abl_stamp<ABL>(a, lane, 4);
+    bytes += valid ? c_len : 0u;
     if (!(ABL & kAblNoStore)) {
         if (ring.n == RS) ring.template flush<true>(a, lane, bc);
         ring.put(s, lane, rec);
     }
+    abl_stamp<ABL>(a, lane, 5);
     s = s1;
     c_off = n_off; c_len = n_len;
     n_off = y_off; n_len = y_len;
@@ -1561,7 +1581,9 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         const uint32_t off = c_off, len = valid ? c_len : 0u;
         const int cls = valid ? size_class(len) : 9;
         if constexpr (MODE != 0) {
-            if (__ballot(cls == 0) == ~0ull) {
+            // (the server: a partial slice whose valid frames are all small too -- a served
+            // burst of fewer than 64 frames is one; its invalid lanes classify nothing)
+            if (__ballot(cls == 0 || (SRV && !valid)) == ~0ull) {
                 // A run of all-small slices (every frame <= 64 bytes; lane i owns frame i end
                 // to end), prefetched one slice deep: the next slice's frame loads are issued
                 // before this slice's are waited for.  vmcnt retires in order, so the loads
@@ -1646,6 +1668,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         n_off = y_off; n_len = y_len;
     }
     if constexpr (MODE != 0) ring.flush(a, lane, bc);
+    abl_stamp<ABL>(a, lane, 6);
 
     if (a.counters == nullptr) return;
     // wave -> workgroup -> one atomic per counter
@@ -1666,6 +1689,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         // replica row per workgroup (rxg.h RXG_COUNTER_ROWS): 32 adders per line, not 2048
         if (v) atomicAdd(&a.counters[(blk % kKernelCounterRows) * RXG_NCOUNTERS + k], v);
     }
+    abl_stamp<ABL>(a, lane, 7);
 }
 
 // One launch per batch (rxg_rx_burst_dev / _bursts_dev / _strided_dev, the replay's
@@ -1725,7 +1749,15 @@ __device__ __forceinline__ uint32_t row_xor16(uint32_t v)
 }
 
 // SRVX (experiment builds, timing only: where a served burst's microseconds go): 1 = no rx
-// body (the protocol alone), 2 = no acquire at the request, 4 = no release before `done`.
+// body (the protocol alone), 2 = no acquire at the request, 4 = no release before `done`,
+// 8 = workgroup 0's thread 0 stamps each request's phases (constant-rate wall clock and the
+// shader clock) into the counters block past its first row (which a one-workgroup server
+// counts in): 8 words per request at 16 + (number mod 64) * 8 -- seen, acquired, body done,
+// stores landed, released, and the shader clock at acquired / released; 16 / 32 / 64 / 128
+// with 8: the body without its TCB probe / its record stores / with cache-resident buckets /
+// without the search (kAblNoProbe / kAblNoStore / kAblHotBuckets / kAblNoSearch); 256 with
+// 8: the body's own phases too (kAblStamps: 8 more words per request after the 64 above);
+// 512 with 8: the body run twice per request, the second end stamped in word 7.
 // Three waves per SIMD at most (168 VGPRs): the pipelined rounds would otherwise take 170.
 template <int MODE, int SRVX = 0>
 __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
@@ -1739,6 +1771,7 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
     // take part in was published, still sees g as new, since g is not done without it.
     unsigned long long last = 0ull;
     if (threadIdx.x == 0) last = __hip_atomic_load(&sa.ret->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned long long stamp[8] = {};  // SRVX & 8 (thread 0 of workgroup 0)
     for (;;) {
         if (blockIdx.x == 0 && threadIdx.x < 64) {
             // wave 0 polls the mailbox's first 320 bytes (lane l < 40: bytes 8l .. 8l+7) in
@@ -1793,8 +1826,13 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
             // (mirror tables, caller frames); waited for before any wave of the workgroup loads
             // (MI355X_MICROARCH.md, inter-workgroup visibility).  A first form with relaxed
             // polls and no acquire served stale staging lines (test_gpu_server).
+            if constexpr ((SRVX & 8) != 0) stamp[0] = (unsigned long long)wall_clock64();
             if constexpr (!(SRVX & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr ((SRVX & 8) != 0) {
+                stamp[1] = (unsigned long long)wall_clock64();
+                stamp[5] = __builtin_amdgcn_s_memtime();
+            }
             // the request's words, written by lanes 1-11, for lane 0
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1870,7 +1908,16 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
         a.b[0].n = uniform(s_req.n);
         a.b[0].slice0 = 0u;
         a.nslices = (a.b[0].n + 63u) / 64u;
-        if constexpr (!(SRVX & 1)) rx_body<MODE, kDescList, false, false, true, 0>(a, blockIdx.x, P);
+        constexpr int ABL = ((SRVX & 16) ? kAblNoProbe : 0) | ((SRVX & 32) ? kAblNoStore : 0) |
+                            ((SRVX & 64) ? kAblHotBuckets : 0) | ((SRVX & 128) ? kAblNoSearch : 0) |
+                            ((SRVX & 256) ? kAblStamps : 0);
+        if constexpr ((SRVX & 256) != 0) a.sel = reinterpret_cast<const uint32_t *>(sa.counters + 16u + 64u * 8u + (q & 63u) * 8u);
+        if constexpr (!(SRVX & 1)) rx_body<MODE, kDescList, false, false, true, ABL>(a, blockIdx.x, P);
+        if constexpr ((SRVX & 8) != 0) stamp[2] = (unsigned long long)wall_clock64();
+        if constexpr ((SRVX & 512) != 0) {  // the body again, its code and data now cached
+            rx_body<MODE, kDescList, false, false, true, ABL>(a, blockIdx.x, P);
+            stamp[7] = (unsigned long long)wall_clock64();
+        }
         // Every wave's stores have reached the L2 (vmcnt), then ONE system-scope release per
         // workgroup writes this XCD's L2 back (buffer_wbl2 covers the whole cache, so one
         // per workgroup covers its four waves; it used to run once per wave and once more
@@ -1878,8 +1925,17 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
+            if constexpr ((SRVX & 8) != 0) stamp[3] = (unsigned long long)wall_clock64();
             if constexpr (!(SRVX & 4)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr ((SRVX & 8) != 0) {
+                stamp[4] = (unsigned long long)wall_clock64();
+                stamp[6] = __builtin_amdgcn_s_memtime();
+                if (blockIdx.x == 0) {
+                    unsigned long long *d = sa.counters + 16u + (q & 63u) * 8u;  // vector stores
+                    for (int k = 0; k < 8; ++k) d[k] = stamp[k];
+                }
+            }
             bool lastp = true;
             if (P > 1u) {
                 lastp = atomicAdd(&sa.ctl->fin, 1u) + 1u == P;
