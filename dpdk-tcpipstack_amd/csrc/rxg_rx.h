@@ -1671,6 +1671,28 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     abl_stamp<ABL>(a, lane, 6);
 
     if (a.counters == nullptr) return;
+    if constexpr (SRV) {
+        // The server: each wave adds its own counts (lanes 0-15, one atomic instruction), with
+        // no workgroup reduction and no 64-bit cross-lane sum -- a served burst is one wave's
+        // latency, and these were 0.75 us of it.  A lane's bytes fit 32 bits
+        // here (a request is at most 2^20 frames: <= 2^14 slices of one frame per lane).
+        uint32_t b = (uint32_t)bytes;
+        b += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x128, 0xF, 0xF, false);  // row_ror:8
+        b += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x124, 0xF, 0xF, false);  // row_ror:4
+        b += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        b += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+        const unsigned long long tot = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)b, 0) +
+                                       (uint32_t)__builtin_amdgcn_readlane((int)b, 16) +
+                                       (uint32_t)__builtin_amdgcn_readlane((int)b, 32) +
+                                       (uint32_t)__builtin_amdgcn_readlane((int)b, 48);
+        uint32_t mine = 0u;
+#pragma unroll
+        for (int k = 0; k < RXG_NCOUNTERS; ++k) mine = lane == k ? wc.c[k] : mine;
+        const unsigned long long v = (MODE != 0 && lane == RXG_C_BYTES) ? tot : (unsigned long long)mine;
+        if (lane < RXG_NCOUNTERS && v) atomicAdd(&a.counters[(blk % kKernelCounterRows) * RXG_NCOUNTERS + lane], v);
+        abl_stamp<ABL>(a, lane, 7);
+        return;
+    }
     // wave -> workgroup -> one atomic per counter
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) {
