@@ -724,11 +724,14 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
 __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int lane, uint32_t *sf,
                                                       uint32_t (&d)[4][4]);
 
+// part / parts: this wave takes rounds part, part + parts, ... of the class (the server's
+// cooperative single slice, rx_body; 0 / 1 everywhere else).
 template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PIPE = false>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
-                                          int lane_in, uint32_t *sf)
+                                          int lane_in, uint32_t *sf, uint32_t part = 0u, uint32_t parts = 1u)
 {
     constexpr int FPW = 64 / LPF;
+    const uint32_t r0 = part * (uint32_t)FPW, step = parts * (uint32_t)FPW;
     const unsigned long long m = __ballot(cls == C);
     if (m == 0ull) return;
     // An opaque copy of the lane id: without it LICM hoists every class's lane-derived
@@ -767,13 +770,13 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             return act;
         };
         uint32_t ao, aoff, alen, bo, boff, blen;
-        bool aact = rmeta(0u, ao, aoff, alen);
+        bool aact = rmeta(r0, ao, aoff, alen);
         round_load<C, LPF, NLOAD, NT>(a, aoff, alen, lane, dA);
         // one loop body, no exit in its middle: the loads of both buffers are issued every
         // iteration and only round B's compute is conditional, so the wait for each buffer
         // counts exactly the other buffer's loads issued after it
-        for (uint32_t r = 0; r < cnt; r += 2u * FPW) {
-            const bool bact = rmeta(r + FPW, bo, boff, blen);
+        for (uint32_t r = r0; r < cnt; r += 2u * step) {
+            const bool bact = rmeta(r + step, bo, boff, blen);
             round_load<C, LPF, NLOAD, NT>(a, boff, blen, lane, dB);
             {
                 const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT>(a, aoff, alen, aact, lane, dA);
@@ -781,9 +784,9 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
                     if (aact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, ao, F);
                 }
             }
-            aact = rmeta(r + 2u * FPW, ao, aoff, alen);
+            aact = rmeta(r + 2u * step, ao, aoff, alen);
             round_load<C, LPF, NLOAD, NT>(a, aoff, alen, lane, dA);
-            if (r + FPW < cnt) {
+            if (r + step < cnt) {
                 const Fields F = frame_round_compute<C, LPF, NLOAD, MODE, NT>(a, boff, blen, bact, lane, dB);
                 if constexpr (MODE != 0) {
                     if (bact && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, bo, F);
@@ -792,7 +795,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
         }
         return;
     }
-    for (uint32_t r = 0; r < cnt; r += FPW) {
+    for (uint32_t r = r0; r < cnt; r += step) {
         const uint32_t k = r + (uint32_t)(lane / LPF);
         const bool act = k < cnt;
         uint32_t korig, koff, klen;
@@ -1574,6 +1577,45 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     BurstCursor<MULTI> bc;
     bc.load(a, lane);
     const uint32_t nslices = a.nslices;
+    // The streaming classes' rounds software-pipelined in tx (MODE 0, 101
+    // VGPRs) and in the server; in launched rx, at the occupancy grid, the second buffer's
+    // register cap cost more than the overlap gained.  Multi-burst kernels keep the plain
+    // form: with the burst table held in lanes the pipelined rounds need 176 VGPRs.
+    constexpr bool PIPE = !MULTI && (MODE == 0 || SRV);
+    // The server's cooperative single slice: a request of one slice on one workgroup (a small
+    // burst) is otherwise one wave's instruction latency, its three other waves idle.  When the
+    // slice is not all small, the four waves share its streaming-class rounds (wave w: rounds
+    // w, w + 4, ...), parking the fields in wave 0's scratch, and wave 0 classifies after a
+    // workgroup barrier.  Slices of at least 8 frames: below that a class
+    // has too few rounds to share, and the barrier would only wait for the idle waves.
+    bool coop = false;
+    if constexpr (SRV && MODE != 0) {
+        if (nblk == 1u && nslices == 1u && slice_frames(a, 0u, bc) >= 8u) {
+            coop = true;
+            if (wid != 0) {
+                uint32_t off0, len0;
+                load_desc<DESC>(a, 0u, lane, off0, len0, bc);
+                const bool valid0 = (uint32_t)lane < slice_frames(a, 0u, bc);
+                const uint32_t l0 = valid0 ? len0 : 0u;
+                const int cls0 = valid0 ? size_class(l0) : 9;
+                if (__ballot(cls0 == 0 || !valid0) != ~0ull) {
+                    uint32_t *sf0 = reinterpret_cast<uint32_t *>(s_rec[0][0]);  // wave 0's ring is empty
+                    const uint32_t w = (uint32_t)wid;
+                    run_class<1, 2, 4, false, MODE, false, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<2, 4, 4, false, MODE, false, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<3, 8, 4, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<10, 8, 5, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<8, 8, 6, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<4, 16, 4, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<5, 16, 6, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<6, 32, 4, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    run_class<7, 64, 2, true, MODE, true>(a, cls0, off0, l0, lane, sf0, w, 4u);
+                    __syncthreads();  // wave 0's, before its phase B
+                }
+                s = nslices;  // nothing more for this wave
+            }
+        }
+    }
     load_desc<DESC>(a, s, lane, c_off, c_len, bc);
     load_desc<DESC>(a, s + nwaves, lane, n_off, n_len, bc);
     while (s < nslices) {
@@ -1632,23 +1674,23 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         load_desc<DESC>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
         // parked fields, and the 4 KiB class-0 transpose after them
         uint32_t *sf = MODE == 0 ? reinterpret_cast<uint32_t *>(ring.img[0]) : ring.scratch(a, lane, NF * 256 + 4096, bc);
-        // The streaming classes' rounds software-pipelined in tx (MODE 0, 101
-        // VGPRs) and in the server; in launched rx, at the occupancy grid, the second buffer's
-        // register cap cost more than the overlap gained.  Multi-burst kernels keep the plain
-        // form: with the burst table held in lanes the pipelined rounds need 176 VGPRs.
-        constexpr bool PIPE = !MULTI && (MODE == 0 || SRV);
+        // (coop: this is wave 0, taking rounds 0, 4, ... of each class)
+        const uint32_t parts = coop ? 4u : 1u;
         // classes 0-2 of mixed slices: plain loads; the larger ones non-temporal (measured
         // +5 % at 1500 B, -4 % at 64 B)
         run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
-        run_class<1, 2, 4, false, MODE, false, PIPE>(a, cls, off, len, lane, sf);
-        run_class<2, 4, 4, false, MODE, false, PIPE>(a, cls, off, len, lane, sf);
-        run_class<3, 8, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
-        run_class<10, 8, 5, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
-        run_class<8, 8, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
-        run_class<4, 16, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
-        run_class<5, 16, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
-        run_class<6, 32, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf);
-        run_class<7, 64, 2, true, MODE, true>(a, cls, off, len, lane, sf);
+        run_class<1, 2, 4, false, MODE, false, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<2, 4, 4, false, MODE, false, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<3, 8, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<10, 8, 5, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<8, 8, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<4, 16, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<5, 16, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<6, 32, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<7, 64, 2, true, MODE, true>(a, cls, off, len, lane, sf, 0u, parts);
+        if constexpr (SRV && MODE != 0) {
+            if (coop) __syncthreads();  // the other waves' parked fields
+        }
         if constexpr (MODE == 0 || (ABL & kAblNoPhaseB)) {
             wcount(wc, RXG_C_RX, valid);
         } else {
