@@ -1577,6 +1577,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     BurstCursor<MULTI> bc;
     bc.load(a, lane);
     const uint32_t nslices = a.nslices;
+    abl_stamp<ABL>(a, lane, 8);
     // The streaming classes' rounds software-pipelined in tx (MODE 0, 101
     // VGPRs) and in the server; in launched rx, at the occupancy grid, the second buffer's
     // register cap cost more than the overlap gained.  Multi-burst kernels keep the plain
@@ -1625,7 +1626,9 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         if constexpr (MODE != 0) {
             // (the server: a partial slice whose valid frames are all small too -- a served
             // burst of fewer than 64 frames is one; its invalid lanes classify nothing)
-            if (__ballot(cls == 0 || (SRV && !valid)) == ~0ull) {
+            const bool all_small = __ballot(cls == 0 || (SRV && !valid)) == ~0ull;
+            abl_stamp<ABL>(a, lane, 9);
+            if (all_small) {
                 // A run of all-small slices (every frame <= 64 bytes; lane i owns frame i end
                 // to end), prefetched one slice deep: the next slice's frame loads are issued
                 // before this slice's are waited for.  vmcnt retires in order, so the loads
@@ -1635,6 +1638,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
                 // register copy of a load in flight would wait for it).
                 uint4 vb[2][4];
                 issue_small_slice<true>(a, c_off, c_len, lane, vb[0]);
+                abl_stamp<ABL>(a, lane, 10);
                 if constexpr (DEEP) {
                     // two-deep: s + nwaves's frames too when that slice is all-small
                     const uint32_t s1 = s + nwaves;
@@ -1816,11 +1820,11 @@ __device__ __forceinline__ uint32_t row_xor16(uint32_t v)
 // body (the protocol alone), 2 = no acquire at the request, 4 = no release before `done`,
 // 8 = workgroup 0's thread 0 stamps each request's phases (constant-rate wall clock and the
 // shader clock) into the counters block past its first row (which a one-workgroup server
-// counts in): 8 words per request at 16 + (number mod 64) * 8 -- seen, acquired, body done,
+// counts in): 8 words per request at 16 + (number mod 32) * 8 -- seen, acquired, body done,
 // stores landed, released, and the shader clock at acquired / released; 16 / 32 / 64 / 128
 // with 8: the body without its TCB probe / its record stores / with cache-resident buckets /
 // without the search (kAblNoProbe / kAblNoStore / kAblHotBuckets / kAblNoSearch); 256 with
-// 8: the body's own phases too (kAblStamps: 8 more words per request after the 64 above);
+// 8: the body's own phases too (kAblStamps: 16 more words per request after the 32 above);
 // 512 with 8: the body run twice per request, the second end stamped in word 7.
 // Three waves per SIMD at most (168 VGPRs): the pipelined rounds would otherwise take 170.
 template <int MODE, int SRVX = 0>
@@ -1975,7 +1979,10 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
         constexpr int ABL = ((SRVX & 16) ? kAblNoProbe : 0) | ((SRVX & 32) ? kAblNoStore : 0) |
                             ((SRVX & 64) ? kAblHotBuckets : 0) | ((SRVX & 128) ? kAblNoSearch : 0) |
                             ((SRVX & 256) ? kAblStamps : 0);
-        if constexpr ((SRVX & 256) != 0) a.sel = reinterpret_cast<const uint32_t *>(sa.counters + 16u + 64u * 8u + (q & 63u) * 8u);
+        if constexpr ((SRVX & 256) != 0) {
+            a.sel = reinterpret_cast<const uint32_t *>(sa.counters + 16u + 32u * 8u + (q & 31u) * 16u);
+            abl_stamp<ABL>(a, (int)(threadIdx.x & 63u), 11);  // the request's words read, RxArgs built
+        }
         if constexpr (!(SRVX & 1)) rx_body<MODE, kDescList, false, false, true, ABL>(a, blockIdx.x, P);
         if constexpr ((SRVX & 8) != 0) stamp[2] = (unsigned long long)wall_clock64();
         if constexpr ((SRVX & 512) != 0) {  // the body again, its code and data now cached
@@ -1996,7 +2003,7 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
                 stamp[4] = (unsigned long long)wall_clock64();
                 stamp[6] = __builtin_amdgcn_s_memtime();
                 if (blockIdx.x == 0) {
-                    unsigned long long *d = sa.counters + 16u + (q & 63u) * 8u;  // vector stores
+                    unsigned long long *d = sa.counters + 16u + (q & 31u) * 8u;  // vector stores
                     for (int k = 0; k < 8; ++k) d[k] = stamp[k];
                 }
             }

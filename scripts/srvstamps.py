@@ -33,13 +33,13 @@ def run(eng, fn, reps=64 * 8):
         a = time.perf_counter()
         fn()
         host.append(time.perf_counter() - a)
-    raw = np.empty(16 + 2 * 64 * 8, dtype=np.uint64)
+    raw = np.empty(16 + 32 * 8 + 32 * 16, dtype=np.uint64)
     # (a request's stamps reach memory with the next request's release: the last slot may be
-    # stale, the medians are over 64)
+    # stale, the medians are over 32)
     eng.d2h(raw.ctypes.data, eng.counters_dev_ptr(), raw.nbytes)
     eng.sync()
-    st = raw[16:16 + 512].reshape(64, 8).astype(np.int64)
-    bs = raw[16 + 512:].reshape(64, 8).astype(np.int64)  # variant 88: the body's phases
+    st = raw[16:16 + 256].reshape(32, 8).astype(np.int64)
+    bs = raw[16 + 256:].reshape(32, 16).astype(np.int64)  # variant 88: the body's phases
     us = lambda a, b: np.median((st[:, b] - st[:, a]) / WALL_MHZ)  # noqa: E731
     span = (st[:, 4] - st[:, 1]) / WALL_MHZ  # us
     mhz = np.median((st[:, 6] - st[:, 5]) / np.maximum(span, 1e-3))
@@ -50,7 +50,7 @@ def run(eng, fn, reps=64 * 8):
         # body phases from the acquire: frames landed + transposed, fields, probe issued,
         # classified, record put, ring flushed, counters
         names = ["step_entry", "frames_in_lds", "fields", "probe_issued", "classified", "rec_put",
-                 "flushed", "counted"]
+                 "flushed", "counted", "body_entry", "all_small_decided", "frames_issued", "args_built"]
         for k, nm in enumerate(names):
             extra[nm + "_us"] = round(float(np.median((bs[:, k] - st[:, 1]) / WALL_MHZ)), 2)
     return {**extra, "host_us": round(float(np.median(host)) * 1e6, 2),
