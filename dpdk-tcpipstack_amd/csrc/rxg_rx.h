@@ -1602,6 +1602,8 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
                 if (__ballot(cls0 == 0 || !valid0) != ~0ull) {
                     uint32_t *sf0 = reinterpret_cast<uint32_t *>(s_rec[0][0]);  // wave 0's ring is empty
                     const uint32_t w = (uint32_t)wid;
+                    // (class 0 is one round of 64 frames and its transpose uses wave 0's LDS:
+                    // wave 0's alone)
                     run_class<1, 2, 4, false, MODE, false, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
                     run_class<2, 4, 4, false, MODE, false, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
                     run_class<3, 8, 4, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);

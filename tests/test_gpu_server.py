@@ -3,6 +3,7 @@ through a mailbox (device memory the host writes through the BAR, or coherent ho
 both placements are tested); its records, counters and replay must equal the launched path's
 and the oracle's, burst after burst (fresh frame content each time: no stale reads of the
 staging), across mirror writes, idle exits and restarts."""
+import random
 import time
 
 import numpy as np
@@ -342,3 +343,40 @@ def test_server_overflow_walks_see_mirror_writes(flags):
     finally:
         _free_all(dev, ref, out)
         eng.close()
+
+
+@pytest.mark.parametrize("flags", PLACEMENTS)
+def test_server_small_bursts_of_every_size_class(srv_engine, flags):
+    """Round 4's server forms for a request of one slice: descriptors
+    carried in the mailbox (host bursts of <= 32 frames), the all-small path for a partial
+    slice of small frames, and the workgroup's four waves sharing the streaming-class rounds
+    of a slice of >= 8 frames.  Bursts of 1..64 frames holding every size class (small, 65-128,
+    .., 1 025-1 536, 1 537-2 048, jumbo) or only small frames, each served, launched and (REC48,
+    every field) run through the oracle: equal."""
+    eng = srv_engine
+    rng = random.Random(404)
+    rows, flows, _ = pktgen.parity_table(rng, 50)
+    tcb, live = pktgen.table_arrays(rows)
+    eng.tcb_load(tcb, live)
+    sizes = [60, 64, 100, 200, 400, 550, 700, 900, 1500, 2000, 4000, 9000]
+    bursts = []
+    for k in [1, 2, 7, 8, 9, 12, 31, 32, 33, 63, 64]:
+        for small_only in (False, True):
+            b = []
+            for i in range(k):
+                L = rng.choice(sizes[:2]) if small_only else sizes[i % len(sizes)] if i < len(sizes) else rng.choice(sizes)
+                src, sport, dport = rng.choice(flows)
+                f = pktgen.frame(src_ip=src, sport=sport, dport=dport, payload=rng.randbytes(max(0, L - 54)),
+                                 flags=rng.choice([0x02, 0x10, 0x18]))
+                b.append(f[:L])
+            bursts.append(b)
+    eng.server_start(rxg.REC48, blocks=1, max_frames=64, flags=flags)
+    try:
+        served = [eng.rx_burst(b, rxg.REC48) for b in bursts]
+    finally:
+        eng.server_stop()
+    for b, got in zip(bursts, served):
+        assert eng.rx_burst(b, rxg.REC48).tobytes() == got.tobytes(), len(b)
+        arena, off, lens = pktgen.pack_arena(b)
+        exp, _ = oracle.rx_batch(arena, off, lens, tcb, live)
+        assert_records_equal(got, exp, b)
