@@ -78,18 +78,23 @@ static int cmp(const void *a, const void *b)
     return (x > y) - (x < y);
 }
 
-/* ITERS bursts, each timed: rxg_rx_burst + rxg_rx_replay; t[] sorted */
+/* ITERS bursts, each timed: rxg_rx_burst + rxg_rx_replay (t), the replay alone (r); sorted */
 static void run(const rxg_pkt_view *views, void **mbufs, void **frames, uint32_t burst, int iters, rxg_rec8 *rec,
-                const rxg_handoff_ops *ops, double *t)
+                const rxg_handoff_ops *ops, double *t, double *r)
 {
     for (int i = -100; i < iters; ++i) {
         const double t0 = now_us();
         if (rxg_rx_burst(g, views, burst, RXG_REC8, rec)) die("rxg_rx_burst");
-        if (rxg_rx_replay(g, ops, mbufs, frames, rec, burst, RXG_REC8)) die("rxg_rx_replay");
         const double t1 = now_us();
-        if (i >= 0) t[i] = t1 - t0;
+        if (rxg_rx_replay(g, ops, mbufs, frames, rec, burst, RXG_REC8)) die("rxg_rx_replay");
+        const double t2 = now_us();
+        if (i >= 0) {
+            t[i] = t2 - t0;
+            r[i] = t2 - t1;
+        }
     }
     qsort(t, (size_t)iters, sizeof *t, cmp);
+    qsort(r, (size_t)iters, sizeof *r, cmp);
 }
 
 int main(int argc, char **argv)
@@ -132,22 +137,25 @@ int main(int argc, char **argv)
     rxg_rec8 *rec = calloc(burst, sizeof *rec);
     rxg_handoff_ops ops = {.free_mbuf = ops_free, .send_reset = ops_rst, .tcpswitch = ops_switch};
     double *ts = malloc(sizeof(double) * (size_t)iters), *tl = malloc(sizeof(double) * (size_t)iters);
+    double *rs = malloc(sizeof(double) * (size_t)iters), *rl = malloc(sizeof(double) * (size_t)iters);
 
     rxg_server_config sc = {RXG_REC8, blocks, burst, burst * ((uint32_t)len + 64u), 0u, 0u};
     if (rxg_server_start(g, &sc) != 0) die("rxg_server_start");
-    run(views, mbufs, frames, burst, iters, rec, &ops, ts);
+    run(views, mbufs, frames, burst, iters, rec, &ops, ts, rs);
     const int placement = rxg_server_placement(g);
     if (rxg_server_stop(g) != 0) die("rxg_server_stop");
     for (uint32_t i = 0; i < burst; ++i)
         if (rec[i].w0 == 0u && rec[i].w1 == 0u) die("empty record");
-    run(views, mbufs, frames, burst, iters, rec, &ops, tl);
+    run(views, mbufs, frames, burst, iters, rec, &ops, tl, rl);
 
     printf("{\"frame_bytes\": %d, \"burst\": %u, \"peers\": %d, \"iters\": %d, \"blocks\": %u, \"placement\": \"%s\", "
            "\"served_us\": {\"p10\": %.2f, \"median\": %.2f, \"p90\": %.2f}, "
-           "\"launched_us\": {\"p10\": %.2f, \"median\": %.2f, \"p90\": %.2f}, \"timing\": \"C, clock_gettime around "
+           "\"launched_us\": {\"p10\": %.2f, \"median\": %.2f, \"p90\": %.2f}, "
+           "\"replay_us_median\": {\"served\": %.2f, \"launched\": %.2f}, \"timing\": \"C, clock_gettime around "
            "rxg_rx_burst + rxg_rx_replay (empty handlers)\"}\n",
            len, burst, peers, iters, blocks, placement == RXG_SRV_DEVICE ? "device" : "host", ts[iters / 10],
-           ts[iters / 2], ts[iters * 9 / 10], tl[iters / 10], tl[iters / 2], tl[iters * 9 / 10]);
+           ts[iters / 2], ts[iters * 9 / 10], tl[iters / 10], tl[iters / 2], tl[iters * 9 / 10], rs[iters / 2],
+           rl[iters / 2]);
     rxg_fini(g);
     return 0;
 }
