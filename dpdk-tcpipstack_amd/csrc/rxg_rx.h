@@ -1583,42 +1583,49 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     // register cap cost more than the overlap gained.  Multi-burst kernels keep the plain
     // form: with the burst table held in lanes the pipelined rounds need 176 VGPRs.
     constexpr bool PIPE = !MULTI && (MODE == 0 || SRV);
-    // The server's cooperative single slice: a request of one slice on one workgroup (a small
-    // burst) is otherwise one wave's instruction latency, its three other waves idle.  When the
-    // slice is not all small, the four waves share its streaming-class rounds (wave w: rounds
-    // w, w + 4, ...), parking the fields in wave 0's scratch, and wave 0 classifies after a
-    // workgroup barrier.  Slices of at least 8 frames: below that a class
-    // has too few rounds to share, and the barrier would only wait for the idle waves.
-    bool coop = false;
+    // The server's cooperative slices: a request of one or two slices on one workgroup (a small
+    // burst) otherwise runs on one or two waves, the others idle.  The workgroup's four waves
+    // share them: slice j (j < ck, the slices) is led by wave j, which classifies it, and the
+    // waves w >= ck help the slice w mod ck, each of the 4 / ck waves of a slice taking its
+    // streaming-class rounds part, part + 4 / ck, ... (part = w / ck), parking the fields in the
+    // leader's scratch; the leader classifies after a workgroup barrier.
+    // Slices of at least 8 frames: below that a class has too few rounds to share, and the
+    // barrier would only wait for the idle waves.  Barriers: one slice -- each wave passes one
+    // when the slice is not all small (the leader on its class path), none otherwise; two
+    // slices -- every wave passes exactly one (a leader after its class path or its all-small
+    // run, a helper after its rounds, whatever its slice holds).
+    uint32_t ck = 0u;
     if constexpr (SRV && MODE != 0) {
-        if (nblk == 1u && nslices == 1u && slice_frames(a, 0u, bc) >= 8u) {
-            coop = true;
-            if (wid != 0) {
-                uint32_t off0, len0;
-                load_desc<DESC>(a, 0u, lane, off0, len0, bc);
-                const bool valid0 = (uint32_t)lane < slice_frames(a, 0u, bc);
-                const uint32_t l0 = valid0 ? len0 : 0u;
-                const int cls0 = valid0 ? size_class(l0) : 9;
-                if (__ballot(cls0 == 0 || !valid0) != ~0ull) {
-                    uint32_t *sf0 = reinterpret_cast<uint32_t *>(s_rec[0][0]);  // wave 0's ring is empty
-                    const uint32_t w = (uint32_t)wid;
-                    // (class 0 is one round of 64 frames and its transpose uses wave 0's LDS:
-                    // wave 0's alone)
-                    run_class<1, 2, 4, false, MODE, false, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<2, 4, 4, false, MODE, false, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<3, 8, 4, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<10, 8, 5, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<8, 8, 6, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<4, 16, 4, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<5, 16, 6, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<6, 32, 4, false, MODE, true, PIPE>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    run_class<7, 64, 2, true, MODE, true>(a, cls0, off0, l0, lane, sf0, w, 4u);
-                    __syncthreads();  // wave 0's, before its phase B
-                }
-                s = nslices;  // nothing more for this wave
+        if (nblk == 1u && (nslices == 1u || nslices == 2u) && slice_frames(a, 0u, bc) >= 8u &&
+            (nslices == 1u || slice_frames(a, 1u, bc) >= 8u))
+            ck = nslices;
+        if (ck != 0u && (uint32_t)wid >= ck) {
+            const uint32_t j = (uint32_t)wid % ck, part = (uint32_t)wid / ck, parts = 4u / ck;
+            uint32_t offj, lenj;
+            load_desc<DESC>(a, j, lane, offj, lenj, bc);
+            const bool validj = (uint32_t)lane < slice_frames(a, j, bc);
+            const uint32_t lj = validj ? lenj : 0u;
+            const int clsj = validj ? size_class(lj) : 9;
+            const bool big = __ballot(clsj == 0 || !validj) != ~0ull;
+            if (big) {
+                uint32_t *sfj = reinterpret_cast<uint32_t *>(s_rec[j][0]);  // the leader's ring is empty
+                // (class 0 is one round of 64 frames and its transpose uses the leader's LDS:
+                // the leader's alone)
+                run_class<1, 2, 4, false, MODE, false, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<2, 4, 4, false, MODE, false, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<3, 8, 4, false, MODE, true, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<10, 8, 5, false, MODE, true, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<8, 8, 6, false, MODE, true, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<4, 16, 4, false, MODE, true, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<5, 16, 6, false, MODE, true, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<6, 32, 4, false, MODE, true, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
+                run_class<7, 64, 2, true, MODE, true>(a, clsj, offj, lj, lane, sfj, part, parts);
             }
+            if (big || ck == 2u) __syncthreads();  // the leaders' (see above)
+            s = nslices;  // nothing more for this wave
         }
     }
+    const bool coop = ck != 0u;
     load_desc<DESC>(a, s, lane, c_off, c_len, bc);
     load_desc<DESC>(a, s + nwaves, lane, n_off, n_len, bc);
     while (s < nslices) {
@@ -1668,6 +1675,9 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
                                                                  vb, ring, wc, rec, fcache, bytes, bc))
                         break;
                 }
+                if constexpr (SRV) {
+                    if (ck == 2u) __syncthreads();  // two cooperative slices: every wave passes one
+                }
                 continue;
             }
         }
@@ -1680,8 +1690,8 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         load_desc<DESC>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
         // parked fields, and the 4 KiB class-0 transpose after them
         uint32_t *sf = MODE == 0 ? reinterpret_cast<uint32_t *>(ring.img[0]) : ring.scratch(a, lane, NF * 256 + 4096, bc);
-        // (coop: this is wave 0, taking rounds 0, 4, ... of each class)
-        const uint32_t parts = coop ? 4u : 1u;
+        // (coop: this wave leads its slice, taking rounds 0, 4 / ck, ... of each class)
+        const uint32_t parts = coop ? 4u / ck : 1u;
         // classes 0-2 of mixed slices: plain loads; the larger ones non-temporal (measured
         // +5 % at 1500 B, -4 % at 64 B)
         run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
