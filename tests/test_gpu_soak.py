@@ -88,3 +88,50 @@ def test_soak_random_launch_shapes():
             e.close()
     print(f"soak: {cases} cases bit-exact")
     assert cases > 0
+
+
+@pytest.mark.skipif(BUDGET <= 0, reason="opt-in soak: set RXG_SOAK=<seconds>")
+def test_soak_served_bursts():
+    """The latency-mode server under random requests (round 4's forms: descriptors in the
+    mailbox, partial all-small slices, one or two slices shared by the workgroup's waves,
+    per-wave counters): random parity batches cut into host bursts of 1..300 frames, served
+    by servers of 1 / 3 / 8 workgroups in every placement, each burst equal to the oracle's
+    records; counters equal the oracle's over the batch."""
+    t_end = time.time() + BUDGET
+    master = random.Random(int(os.environ.get("RXG_SOAK_SEED", "2027")))
+    cases, t_print = 0, time.time()
+    eng = rxg.Engine(device=0, max_batch=1 << 12, max_bytes=16 << 20)
+    try:
+        while time.time() < t_end:
+            seed = master.randrange(1 << 30)
+            rng = random.Random(seed)
+            rows, frames = pktgen.parity_set(seed=seed, n=rng.choice([64, 300, 1000]), nflows=rng.choice([3, 50, 400]))
+            tcb, live = pktgen.table_arrays(rows)
+            kind = rng.choice([rxg.REC8, rxg.REC16, rxg.REC48])
+            blocks = rng.choice([1, 3, 8])
+            flags = rng.choice([0, rxg.SRV_HOST_STAGING, rxg.SRV_HOST_MAILBOX])
+            arena, off, lens = pktgen.pack_arena(frames)
+            exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+            exp = exp if kind == rxg.REC48 else exp["c"] if kind == rxg.REC16 else rxg.rec8_pack(exp["c"])
+            eng.tcb_load(tcb, live)
+            eng.counters_reset()
+            eng.server_start(kind, blocks=blocks, max_frames=512, flags=flags)
+            try:
+                i, got = 0, []
+                while i < len(frames):
+                    k = min(len(frames) - i, rng.choice([1, 2, 7, 8, 31, 32, 33, 63, 64, 65, 100, 128, 129, 300]))
+                    got.append(eng.rx_burst(frames[i:i + k], kind))
+                    i += k
+            finally:
+                eng.server_stop()
+            got = np.concatenate(got)
+            assert got.tobytes() == exp.tobytes(), f"seed {seed} kind {kind} blocks {blocks} flags {flags}"
+            assert eng.counters().tolist() == ecnt.tolist(), f"seed {seed}: counters differ"
+            cases += 1
+            if time.time() - t_print > 20:
+                print(f"served soak: {cases} batches", flush=True)
+                t_print = time.time()
+    finally:
+        eng.close()
+    print(f"served soak: {cases} batches bit-exact")
+    assert cases > 0
