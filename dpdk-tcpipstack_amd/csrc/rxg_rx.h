@@ -1861,7 +1861,9 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
             const unsigned long long lst = __shfl(last, 0, 64);
             const long long t0 = wall_clock64();
             unsigned long long q;
+            uint32_t polls = 0u;  // (SRVX & 256: the poll loop's iterations, stamped)
             for (;;) {
+                if constexpr ((SRVX & 256) != 0) ++polls;
                 unsigned long long w = 0ull;
                 if (l < kSrvPollWords)
                     w = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(sa.mbox) + l, __ATOMIC_RELAXED,
@@ -1907,6 +1909,13 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
             // (MI355X_MICROARCH.md, inter-workgroup visibility).  A first form with relaxed
             // polls and no acquire served stale staging lines (test_gpu_server).
             if constexpr ((SRVX & 8) != 0) stamp[0] = (unsigned long long)wall_clock64();
+            if constexpr ((SRVX & 256) != 0) {
+                if (l == 0 && q != kSrvStop) {  // the poll loop's start and iterations
+                    unsigned long long *d = sa.counters + 16u + 32u * 8u + (q & 31u) * 16u;
+                    d[12] = (unsigned long long)t0;
+                    d[13] = polls;
+                }
+            }
             if constexpr (!(SRVX & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if constexpr ((SRVX & 8) != 0) {

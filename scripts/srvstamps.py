@@ -53,6 +53,9 @@ def run(eng, fn, reps=64 * 8):
                  "flushed", "counted", "body_entry", "all_small_decided", "frames_issued", "args_built"]
         for k, nm in enumerate(names):
             extra[nm + "_us"] = round(float(np.median((bs[:, k] - st[:, 1]) / WALL_MHZ)), 2)
+        polls = np.maximum(bs[:, 13], 1)
+        extra["polls_median"] = int(np.median(bs[:, 13]))
+        extra["poll_iteration_us"] = round(float(np.median((st[:, 0] - bs[:, 12]) / WALL_MHZ / polls)), 3)
     return {**extra, "host_us": round(float(np.median(host)) * 1e6, 2),
             "acquire_us": round(float(us(0, 1)), 2), "body_us": round(float(us(1, 2)), 2),
             "stores_landed_us": round(float(us(2, 3)), 2), "release_us": round(float(us(3, 4)), 2),
