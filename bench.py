@@ -561,6 +561,25 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
             "replicas": multi}
 
 
+def cpu_baseline_per_packet(arena, off, lens, tcb, live, opt, shipped, budget=1.0):
+    """The CPU baseline per packet at the reference's call site (scripts/crossover.py, DESIGN.md
+    §6.R3a): the faithful oracle (-O0 / -O2; shipped = the reference's rx checksum compiled
+    out, tcp_in.c:37) over the given frames in bursts of 64, after one pass has taught its ARP
+    list their sources; microseconds per packet on one host core."""
+    import oracle
+    oracle.arp_reset()
+    oracle.rx_batch(arena, off, lens, tcb, live, faithful=True, opt=opt, shipped=shipped)  # learn ARP
+    n, pk, s, t0 = len(lens), 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget or pk == 0:
+        e = min(s + 64, n)
+        oracle.rx_batch(arena, off[s:e], lens[s:e], tcb, live, faithful=True, opt=opt, shipped=shipped)
+        pk += e - s
+        s = 0 if e >= n else e
+    dt = time.perf_counter() - t0
+    oracle.arp_reset()
+    return dt / pk * 1e6
+
+
 def cpu_replicas(arena, off, lens, tcb, live, cores, seconds):
     """one independent replica of the faithful oracle (-O0) per host
     core, each its own process with private tables, on disjoint ranges of the sample.

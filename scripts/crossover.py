@@ -6,7 +6,8 @@ rxg side, per burst of n host frames: rxg_rx_burst (views -> pinned staging -> H
 kernel -> D2H records, synchronous) + rxg_rx_replay with empty handlers (the handlers are
 the stack's own functions on both sides, so they cancel).  Timed directly at every n.
 
-CPU side: the oracle's faithful restatement of the reference path (ARP list walks with
+CPU side: bench.py's CPU-baseline leg (cpu_baseline_per_packet: the oracle's faithful
+restatement of the reference path, the only place outside tests/ that runs it) (ARP list walks with
 their disabled-logger calls, two-pass linear findtcb with one logger call per scanned TCB,
 malloc + memcpy pseudo header and byte-loop checksum), built -O0 (tcp_ip_stack/Makefile:50)
 and -O2, in two forms: "shipped" (the reference as it ships: no rx checksum, tcp_in.c:37
@@ -31,7 +32,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")]
 import torch  # noqa: E402,F401
-import oracle  # noqa: E402
+import bench  # noqa: E402  (its CPU-baseline leg times the reference path)
 import rxg  # noqa: E402
 
 BURSTS = [32, 256, 4096, 65536]
@@ -57,20 +58,6 @@ def rxg_burst_us(eng, lib, views, ptrs, out, n, budget=0.4):
         dt = time.perf_counter() - t0
         if dt > budget and it >= 5:
             return dt / it * 1e6
-
-
-def cpu_pkt_us(arena, off, lens, tcb, live, opt, shipped, budget=1.0):
-    oracle.arp_reset()
-    oracle.rx_batch(arena, off, lens, tcb, live, faithful=True, opt=opt, shipped=shipped)  # learn ARP
-    n, pk, s, t0 = len(lens), 0, 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget or pk == 0:
-        e = min(s + 64, n)
-        oracle.rx_batch(arena, off[s:e], lens[s:e], tcb, live, faithful=True, opt=opt, shipped=shipped)
-        pk += e - s
-        s = 0 if e >= n else e
-    dt = time.perf_counter() - t0
-    oracle.arp_reset()
-    return dt / pk * 1e6
 
 
 def main():
@@ -107,7 +94,7 @@ def main():
             for opt in (() if no_cpu else ("O0", "O2")):
                 for shipped in (True, False):
                     cpu[f"{opt}_{'shipped' if shipped else 'verify'}"] = round(
-                        cpu_pkt_us(arena, off[:sample], lens[:sample], tcb, live, opt, shipped), 4)
+                        bench.cpu_baseline_per_packet(arena, off[:sample], lens[:sample], tcb, live, opt, shipped), 4)
             row = {"frame_bytes": size, "flows": flows, "tcbs": flows + 1,
                    "rxg_burst_plus_replay_us": g,
                    "server_burst_plus_replay_us": {f"{b}wg": v for b, v in srv.items()},
