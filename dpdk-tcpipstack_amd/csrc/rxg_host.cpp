@@ -1189,11 +1189,12 @@ extern "C" int rxg_server_placement(rxg_ctx *c)
 
 // A served burst.  inl: a host burst of at most kSrvInline frames whose descriptors the
 // request carries in the mailbox (S.idesc, filled by the caller) as well as in the staging.
-static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl);
+// large: a host burst holding a frame over 64 bytes (kSrvLarge).
+static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl, bool large);
 
-extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b) { return server_burst(c, b, false); }
+extern "C" int rxg_server_burst_dev(rxg_ctx *c, const rxg_dev_batch *b) { return server_burst(c, b, false, false); }
 
-static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl)
+static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl, bool large)
 {
     if (!c || !b) return fail(-EINVAL, "rxg_server_burst_dev: NULL argument");
     if (!c->srv.on) return fail(-ENODEV, "rxg_server_burst_dev: no server (rxg_server_start)");
@@ -1219,7 +1220,7 @@ static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl)
         r.len = b->len;
         r.out = (uint8_t *)b->out;
         r.n = b->n;
-        r.flags = inl && b->n <= kSrvInline ? kSrvInlineDesc : 0u;
+        r.flags = (inl && b->n <= kSrvInline ? kSrvInlineDesc : 0u) | (large ? kSrvLarge : 0u);
         r.table = table_view(c);
         if ((rc = srv_post(c, r))) return rc;
     }
@@ -1259,9 +1260,10 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
         // latency mode: packed into the server's coherent staging, served without a launch
         rxg_ctx::Server &S = c->srv;
         uint64_t slot = 0;
-        bool fits = true;
+        bool fits = true, large = false;
         for (uint32_t i = 0; i < n && fits; ++i) {
             const uint64_t need = (pkts[i].data_len + 63u) / 64u;
+            large |= pkts[i].data_len > 64u;
             fits = (slot + need) * 64u <= S.max_bytes;
             S.h_off[i] = (uint32_t)slot;
             S.h_len[i] = pkts[i].data_len;
@@ -1292,7 +1294,7 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
             b.n = n;
             b.rec_kind = rec_kind;
             b.out = S.out;
-            int rc = server_burst(c, &b, inl);
+            int rc = server_burst(c, &b, inl, large);
             if (rc) return rc;
             std::memcpy(out_host, S.out, (size_t)n * rec_kind);
             return 0;

@@ -77,7 +77,8 @@ struct SrvReq {
     const uint16_t *len;
     uint8_t *out;            // records of the server's kind
     uint32_t n;
-    uint32_t flags;          // kSrvInlineDesc: the descriptors are in the mailbox (SrvMbox::ioff / ilen)
+    uint32_t flags;          // kSrvInlineDesc: the descriptors are in the mailbox (SrvMbox::ioff / ilen);
+                             // kSrvLarge: a frame over 64 bytes (host bursts)
     DevTable table;          // the mirror as of the post
 };
 // Host bursts of up to kSrvInline frames carry their descriptors in the mailbox, on the lines
@@ -85,6 +86,9 @@ struct SrvReq {
 // (one dependent device-memory trip less per served burst).
 constexpr uint32_t kSrvInline = 32;
 constexpr uint32_t kSrvInlineDesc = 1u;
+// A host burst holding a frame over 64 bytes: a request of 3..gridDim slices then runs one
+// slice per workgroup, each shared by the workgroup's four waves (rx_body).
+constexpr uint32_t kSrvLarge = 2u;
 // Device memory written through the BAR (large-BAR GPUs, whole lines per post) or coherent
 // host memory; `done` / `exited` are read from the server's return block (host memory, may
 // be a second SrvMbox).  The first 320 bytes (words 0-39) are what the host writes and the

@@ -1594,13 +1594,21 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     // when the slice is not all small (the leader on its class path), none otherwise; two
     // slices -- every wave passes exactly one (a leader after its class path or its all-small
     // run, a helper after its rounds, whatever its slice holds).
-    uint32_t ck = 0u;
+    // One slice per workgroup (srv_participants with kSrvLarge: 3..gridDim slices on as many
+    // workgroups): workgroup blk's slice is blk, led by its wave 0 and shared as one slice is.
+    uint32_t ck = 0u, j0 = 0u;
     if constexpr (SRV && MODE != 0) {
         if (nblk == 1u && (nslices == 1u || nslices == 2u) && slice_frames(a, 0u, bc) >= 8u &&
             (nslices == 1u || slice_frames(a, 1u, bc) >= 8u))
             ck = nslices;
+        if (nblk >= 3u && nslices == nblk) {
+            j0 = blk;
+            if (wid == 0) s = blk;  // (below 8 frames it runs its slice alone)
+            else if (slice_frames(a, blk, bc) < 8u) s = nslices;
+            if (slice_frames(a, blk, bc) >= 8u) ck = 1u;
+        }
         if (ck != 0u && (uint32_t)wid >= ck) {
-            const uint32_t j = (uint32_t)wid % ck, part = (uint32_t)wid / ck, parts = 4u / ck;
+            const uint32_t j = j0 + (uint32_t)wid % ck, part = (uint32_t)wid / ck, parts = 4u / ck;
             uint32_t offj, lenj;
             load_desc<DESC>(a, j, lane, offj, lenj, bc);
             const bool validj = (uint32_t)lane < slice_frames(a, j, bc);
@@ -1608,7 +1616,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
             const int clsj = validj ? size_class(lj) : 9;
             const bool big = __ballot(clsj == 0 || !validj) != ~0ull;
             if (big) {
-                uint32_t *sfj = reinterpret_cast<uint32_t *>(s_rec[j][0]);  // the leader's ring is empty
+                uint32_t *sfj = reinterpret_cast<uint32_t *>(s_rec[j - j0][0]);  // the leader's ring is empty
                 // (class 0 is one round of 64 frames and its transpose uses the leader's LDS:
                 // the leader's alone)
                 run_class<1, 2, 4, false, MODE, false, PIPE>(a, clsj, offj, lj, lane, sfj, part, parts);
@@ -1811,9 +1819,11 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v)
 }
 
 // workgroups a request of n frames runs on
-__device__ __forceinline__ uint32_t srv_participants(uint32_t n)
+__device__ __forceinline__ uint32_t srv_participants(uint32_t n, uint32_t flags)
 {
     const uint32_t nsl = (n + 63u) / 64u;
+    // large frames, 3..gridDim slices: one slice per workgroup (rx_body's shared slices)
+    if ((flags & kSrvLarge) && nsl >= 3u && nsl <= gridDim.x) return nsl;
     return max(1u, min(gridDim.x, (nsl + 3u) / 4u));
 }
 
@@ -1927,7 +1937,7 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (l == 0) {
-                const uint32_t P = q == kSrvStop ? gridDim.x : srv_participants(s_req.n);
+                const uint32_t P = q == kSrvStop ? gridDim.x : srv_participants(s_req.n, s_req.flags);
                 // the others hear of a request only when they take part in it (and of stop)
                 if (gridDim.x > 1 && P > 1u) {
                     if (q != kSrvStop) sa.ctl->req = s_req;
