@@ -1187,6 +1187,29 @@ extern "C" int rxg_server_placement(rxg_ctx *c)
     return c->srv.dev ? RXG_SRV_DEVICE : RXG_SRV_HOST;
 }
 
+// One frame into the server's device staging (write-combined, through the BAR): 32-byte
+// non-temporal stores, the tail from a zero-padded copy (no read past the frame; the slot is
+// 64-byte aligned and as long as the frame rounded up to 64).  Measured against memcpy
+// (scripts/barcopy.cpp, profiles/r04/barcopy/): 32 x 64 B 0.45 -> 0.24 us, 32 x 1 500 B
+// 1.80 -> 1.37, 256 x 1 500 B 12.6 -> 10.1.
+__attribute__((target("avx2"))) static void stage_frame_avx2(uint8_t *d, const uint8_t *s, uint32_t len)
+{
+    uint32_t k = 0;
+    for (; k + 32u <= len; k += 32u)
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + k), _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + k)));
+    if (k < len) {
+        alignas(32) uint8_t t[32] = {};
+        std::memcpy(t, s + k, len - k);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + k), _mm256_load_si256(reinterpret_cast<const __m256i *>(t)));
+    }
+}
+
+static bool host_avx2()
+{
+    static const bool v = __builtin_cpu_supports("avx2");
+    return v;
+}
+
 // A served burst.  inl: a host burst of at most kSrvInline frames whose descriptors the
 // request carries in the mailbox (S.idesc, filled by the caller) as well as in the staging.
 // large: a host burst holding a frame over 64 bytes (kSrvLarge).
@@ -1272,10 +1295,16 @@ extern "C" int rxg_rx_burst(rxg_ctx *c, const rxg_pkt_view *pkts, uint32_t n, ui
         if (fits) {
             // write-only streams into the staging (device memory: write-combined, never read
             // back by the host); srv_post fences them before the request
-            for (uint32_t i = 0; i < n; ++i)
-                if (pkts[i].data_len)
-                    std::memcpy(S.arena + (uint64_t)S.h_off[i] * 64u,
-                                (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off, pkts[i].data_len);
+            const bool stream = S.dev && host_avx2();
+            for (uint32_t i = 0; i < n; ++i) {
+                if (!pkts[i].data_len) continue;
+                uint8_t *d = S.arena + (uint64_t)S.h_off[i] * 64u;
+                const uint8_t *src = (const uint8_t *)pkts[i].buf_addr + pkts[i].data_off;
+                if (stream)
+                    stage_frame_avx2(d, src, pkts[i].data_len);
+                else
+                    std::memcpy(d, src, pkts[i].data_len);
+            }
             // (the staged descriptors are also what a re-classification or a payload gather
             // of this burst reads)
             std::memcpy(S.off, S.h_off.data(), (size_t)n * 4u);
