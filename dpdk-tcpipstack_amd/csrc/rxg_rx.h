@@ -1712,9 +1712,11 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         run_class<5, 16, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
         run_class<6, 32, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
         run_class<7, 64, 2, true, MODE, true>(a, cls, off, len, lane, sf, 0u, parts);
+        abl_stamp<ABL>(a, lane, 12);
         if constexpr (SRV && MODE != 0) {
             if (coop) __syncthreads();  // the other waves' parked fields
         }
+        abl_stamp<ABL>(a, lane, 13);
         if constexpr (MODE == 0 || (ABL & kAblNoPhaseB)) {
             wcount(wc, RXG_C_RX, valid);
         } else {
@@ -1723,6 +1725,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             classify_store<MODE, SRV, ABL>(a, valid, len, unpark_fields<MODE>(sf, lane), wc, rec, fcache, sf + NF * 64);
+            abl_stamp<ABL>(a, lane, 14);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
             if (!(ABL & kAblNoStore)) {
                 if (ring.n == RS) ring.flush(a, lane, bc);

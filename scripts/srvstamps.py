@@ -50,7 +50,8 @@ def run(eng, fn, reps=64 * 8):
         # body phases from the acquire: frames landed + transposed, fields, probe issued,
         # classified, record put, ring flushed, counters
         names = ["step_entry", "frames_in_lds", "fields", "probe_issued", "classified", "rec_put",
-                 "flushed", "counted", "body_entry", "all_small_decided", "frames_issued", "args_built"]
+                 "flushed", "counted", "body_entry", "all_small_decided", "frames_issued", "args_built",
+                 "class_rounds_done", "class_barrier_passed", "class_classified"]
         for k, nm in enumerate(names):
             extra[nm + "_us"] = round(float(np.median((bs[:, k] - st[:, 1]) / WALL_MHZ)), 2)
         polls = np.maximum(bs[:, 13], 1)
@@ -67,9 +68,10 @@ def main():
         sys.exit("srvstamps.py: run with RXG_LIB=<librxg_exp.so> RXG_VARIANT=83 (84: no probe, 85: no stores, "
                  "86: cache-resident buckets, 87: no search, 88: the body's phases, 89: the body twice)")
     n = 256
-    eng = rxg.Engine(0, max_batch=n, max_bytes=n * 1536)
+    eng = rxg.Engine(0, max_batch=n, max_bytes=n * 2048)
     lib = rxg.load_library()
-    b = eng.synth(n=n, nflows=1000, len_a=64, seed=5)
+    size = int(os.environ.get("SRVSTAMPS_FRAME", "64"))  # 1500: the class path (the leader and its helpers)
+    b = eng.synth(n=n, nflows=1000, len_a=size, seed=5)
     eng.sync()
     off = b["off64"].download(np.uint32, n)
     lens = b["len"].download(np.uint16, n)
@@ -83,9 +85,9 @@ def main():
     eng.server_start(rxg.REC8, blocks=1, max_frames=n)
     place = {rxg.SRV_DEVICE: "device", rxg.SRV_HOST: "host"}[eng.server_placement()]
     dref = C.byref(rxg.DevBatch(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, 32, rxg.REC8, d_out.ptr))
-    for name, fn in (("host_32x64B_inline", lambda: lib.rxg_rx_burst(eng.ctx, views, 32, rxg.REC8, out_p)),
-                     ("host_33x64B", lambda: lib.rxg_rx_burst(eng.ctx, views, 33, rxg.REC8, out_p)),
-                     ("dev_32x64B", lambda: lib.rxg_server_burst_dev(eng.ctx, dref))):
+    for name, fn in ((f"host_32x{size}B_inline", lambda: lib.rxg_rx_burst(eng.ctx, views, 32, rxg.REC8, out_p)),
+                     (f"host_33x{size}B", lambda: lib.rxg_rx_burst(eng.ctx, views, 33, rxg.REC8, out_p)),
+                     (f"dev_32x{size}B", lambda: lib.rxg_server_burst_dev(eng.ctx, dref))):
         row = {"case": name, "variant": int(os.environ["RXG_VARIANT"]), "placement": place}
         row.update(run(eng, fn))
         print(json.dumps(row), flush=True)
