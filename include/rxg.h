@@ -418,8 +418,9 @@ int rxg_rx_burst(rxg_ctx *ctx, const rxg_pkt_view *pkts, uint32_t n, uint32_t re
    rxg_rx_burst sends bursts of up to max_frames frames (max_bytes staged bytes) and of
    record kind rec_kind through it (packed into the server's own staging), and
    rxg_server_burst_dev serves device-visible batches.  Records, counters, replay and
-   payload gather are those of the launched path.  A burst of up to 64 frames runs on the
-   first workgroup (its four waves sharing a slice of large frames); with `blocks` >= 3 a host
+   payload gather are those of the launched path.  A burst of up to 128 frames runs on the
+   first workgroup (its four waves sharing one or two 64-frame slices of large frames); with
+   `blocks` >= 3 a host
    burst of 129..64*blocks frames holding a frame over 64 bytes runs one 64-frame slice per
    workgroup, so `blocks` = 4 serves the reference's bursts and bursts of up to 256 large
    frames at the shortest latency.  The server exits by itself after idle_ms
