@@ -42,9 +42,10 @@ TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.jso
                  ("c2_64B_1flow", 1 << 20, 8): "profiles/r04/c2/traffic.json",
                  ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r04/c4/traffic.json",
                  ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r04/c2multi/traffic.json",
-                 # the 8(f) kernels over the headline's C3 batch (scripts/gpu_prof.sh tx3 / pg3)
-                 ("tx_generate_dev", 1 << 20, 8): "profiles/r03/final/tx3/traffic.json",
-                 ("payload_gather", 1 << 20, 8): "profiles/r03/final/pg3/traffic.json",
+                 # the 8(f) kernels over the headline's C3 batch (REC=8 scripts/gpu_prof.sh r05a tx3 pg3, this tree)
+                 ("tx_generate_dev", 1 << 20, 8): "profiles/r05/tx3/traffic.json",
+                 ("payload_gather", 1 << 20, 8): "profiles/r05/pg3/traffic.json",
+                 ("c3_rx_payload_fused", 1 << 20, 8): "profiles/r05/pf3/traffic.json",
                  # round 4: the fixed-stride forms (rxg_rx_bursts_strided_dev), scripts/gpu_prof.sh c2s c2multis
                  ("c2_64B_1flow_strided", 1 << 20, 8): "profiles/r04/c2s/traffic.json",
                  ("c2_64B_1flow_multiburst_strided", 1 << 20, 8): "profiles/r04/c2multis/traffic.json"}
@@ -77,9 +78,15 @@ def shard_seed(base: int, rank: int) -> int:
     return (base * 1_000_003 + rank * 7919 + 1) & 0xFFFFFFFFFFFF
 
 
+def _pg() -> bool:
+    """A process group exists: every helper below runs its collective through it, at world
+    size 1 too (--pg nccl: the RCCL path exercised on one GPU)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def merge_counters(counters: np.ndarray, device) -> np.ndarray:
     """Sum the per-GPU counters over ranks (RCCL all-reduce on GPU, gloo on CPU)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _pg():
         return counters.copy()
     t = torch.from_numpy(counters.astype(np.int64)).to(device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -87,7 +94,7 @@ def merge_counters(counters: np.ndarray, device) -> np.ndarray:
 
 
 def max_over_ranks(x: float, device) -> float:
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _pg():
         return x
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -95,7 +102,7 @@ def max_over_ranks(x: float, device) -> float:
 
 
 def min_over_ranks(x: float, device) -> float:
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _pg():
         return x
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -103,7 +110,7 @@ def min_over_ranks(x: float, device) -> float:
 
 
 def sum_over_ranks(x: float, device) -> float:
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _pg():
         return x
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -111,7 +118,7 @@ def sum_over_ranks(x: float, device) -> float:
 
 
 def barrier(device):
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _pg():
         dist.barrier()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
@@ -416,6 +423,50 @@ def payload_leg(eng, wl, steps, warmup):
             d.free()
 
 
+def fused_leg(eng, wl, steps, warmup):
+    """The burst and its payload hand-off in ONE pass (rxg_rx_burst_payload_dev, DESIGN.md
+    §5.F) over the workload's rotating batches, against the two-pass form (rxg_rx_burst_dev,
+    then rxg_payload_gather_dev reading every payload byte again).  One event pair around the
+    launches.  Algorithmic bytes per launch = the frame bytes read + the payload bytes handed
+    off + a 16-byte message and a record per frame (the two-pass form moves the same plus
+    the payload read a second time)."""
+    arenas = [eng.alloc(b["arena_bytes"]) for b in wl.batches]
+    msgs = eng.alloc(wl.n * 16)
+    pl = (wl.lens.astype(np.int64) - 54).clip(min=0)  # synthetic frames: IHL 5, data_off 5
+    dl = int(pl.sum())
+    try:
+        def launch(i):
+            b = wl.batches[i % wl.copies]
+            eng.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, wl.n, wl.out.ptr,
+                                     arenas[i % wl.copies].ptr, msgs.ptr, wl.rec)
+        for i in range(warmup):
+            launch(i)
+        eng.sync()
+        eng.counters_reset()
+        e0, e1 = eng.event(), eng.event()
+        eng.record(e0)
+        for i in range(steps):
+            launch(warmup + i)
+        eng.record(e1)
+        eng.sync()
+        k = eng.elapsed_ms(e0, e1) / steps / 1e3
+        eng.event_destroy(e0)
+        eng.event_destroy(e1)
+        c = eng.counters()
+        m = msgs.download(rxg.PAYLOAD_MSG_DTYPE, wl.n)
+        alg = wl.bytes_per_batch + dl + (16 + wl.rec) * wl.n
+        tb = traffic_of("c3_rx_payload_fused", wl.n, wl.rec)[0] if wl.name == "c3_1500B_1Kflows" else None
+        return {"kernel_us": round(k * 1e6, 2), "mpps": round(wl.n / k / 1e6, 1),
+                "payload_bytes": dl, "algorithmic_bytes_per_launch": alg,
+                "traffic_bytes_per_launch": tb,
+                "achieved_GBps": round(alg / k / 1e9, 1), "roofline_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4),
+                "ok": bool(int(c[0]) == wl.n * steps and int(c[13]) == wl.n * steps and int(c[8]) == 0
+                           and (m["len"] == pl).all())}
+    finally:
+        for d in arenas + [msgs]:
+            d.free()
+
+
 def tx_leg(eng, wl, steps, warmup):
     """tx checksum generate (rxg_tx_cksum_dev, what ip_out computes,
     ip.c:97-118) over the device-resident batch of the workload, in place.  The frames'
@@ -439,7 +490,13 @@ def tx_leg(eng, wl, steps, warmup):
             "roofline_frac": round(wl.bytes_per_batch / k / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def replay_churn_leg():
+# Rank 0 runs the replay_churn and small_burst legs alone while the other ranks wait at the
+# next barrier: together they may take at most this long (subprocess time limits), far below
+# --pg-timeout, so no waiting rank's collective can time out on them.
+SOLO_BUDGET_S = 180.0
+
+
+def replay_churn_leg(deadline=None):
     """SURVEY.md 8(f) row 2 under load: burst + in-order replay (rxg_rx_replay) with C
     handlers shaped like tcp_states.c's, 1 % of the frames starting a connection event (a new
     client's SYN + ACK: tcp_listen appends a child, tcp_syn_rcv establishes it; or an
@@ -451,10 +508,17 @@ def replay_churn_leg():
     if not os.path.exists(exe):
         return None
     out = {}
+    deadline = deadline or time.perf_counter() + SOLO_BUDGET_S
     for nflows in (65536, 1 << 20):
         for permille in (0, 10):
-            r = subprocess.run([exe, str(nflows), "4096", "40", str(permille)], capture_output=True,
-                               text=True, timeout=300)
+            left = deadline - time.perf_counter()
+            if left < 5:
+                return dict(out, error="solo-leg budget spent")
+            try:
+                r = subprocess.run([exe, str(nflows), "4096", "40", str(permille)], capture_output=True,
+                                   text=True, timeout=left)
+            except subprocess.TimeoutExpired:
+                return dict(out, error=f"churn_bench exceeded the solo-leg budget ({SOLO_BUDGET_S:g} s)")
             if r.returncode != 0:
                 return {"error": r.stderr.strip()[-300:]}
             d = json.loads(r.stdout)
@@ -550,14 +614,30 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
     mpps0, gbs0, pk0, dt0 = res["O0"]
     mpps2, gbs2, pk2, dt2 = res["O2"]
     multi = cpu_replicas(arena, off, lens, tcb, live, cores, seconds * 0.5) if cores > 1 else None
+    # SURVEY.md §6 timed the reference's own hot-path files on this shape (1 500 B, 1 000 flows /
+    # 1 000 source IPs, +verify) in the survey's session: 0.0121 Mpps at -O0, 0.0185 at -O2.
+    # The port runs ~1.3-1.5x slower than those figures; no slower construct was found in its
+    # code (its logger is a direct call; the reference's as a separate
+    # translation unit measured slower still), so the factor is stated, not hidden: a
+    # GPU-over-CPU ratio against `value` may be inflated by it.
+    ref = {"O0": 0.0121, "O2": 0.0185}
+    calib = None
+    if wl.name == "c3_1500B_1Kflows":
+        calib = {"survey_reference_mpps": ref, "shape": "1500 B, 1000 flows / 1000 src IPs, +verify (SURVEY.md §6)",
+                 "reference_over_port": {"O0": round(ref["O0"] / mpps0, 3) if mpps0 else None,
+                                         "O2": round(ref["O2"] / mpps2, 3) if mpps2 else None}}
     return {"value": round(gbs0, 6), "unit": "GB/s", "mpps": round(mpps0, 6), "cores": 1,
             "kind": "port",
             "sample": (f"faithful oracle (reference algorithms: byte-loop checksum, malloc+memcpy "
                        f"pseudo header, two-pass linear findtcb over {wl.flows + 1} TCBs, ARP list "
                        f"walks, disabled-logger calls) built -O0 like tcp_ip_stack/Makefile:50, "
                        f"{pk0} frames of this workload in {dt0:.1f} s on 1 core; "
-                       f"-O2 build: {mpps2:.4f} Mpps / {gbs2:.4f} GB/s"),
+                       f"-O2 build: {mpps2:.4f} Mpps / {gbs2:.4f} GB/s"
+                       + (f"; the reference's own files ran {calib['reference_over_port']['O0']}x (-O0) / "
+                          f"{calib['reference_over_port']['O2']}x (-O2) this port's rate on this shape in "
+                          f"SURVEY.md §6's session (calibration)" if calib else "")),
             "o2": {"mpps": round(mpps2, 6), "gbs": round(gbs2, 6)},
+            "calibration": calib,
             "replicas": multi}
 
 
@@ -631,6 +711,28 @@ def spawn_ranks(ngpus: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def pg_backend(pg: str, world: int, rehearse: bool):
+    """The process group's backend, or None for no process group (--pg auto at world 1)."""
+    if pg == "auto":
+        return None if world == 1 else ("gloo" if rehearse else "nccl")
+    return pg
+
+
+def init_pg(backend: str, rank: int, world: int, timeout_s: float) -> None:
+    """init_process_group with an explicit timeout: no collective (and no rank waiting at a
+    barrier for rank 0's solo legs) waits longer than timeout_s.  At world 1 without a
+    launcher the rendezvous is this process alone, on 127.0.0.1."""
+    import datetime
+    if "MASTER_ADDR" not in os.environ:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(_free_port())
+    os.environ.setdefault("RANK", str(rank))
+    os.environ.setdefault("WORLD_SIZE", str(world))
+    dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s))
+
+
 def rank_devices(gpu: int, have_gpu: bool, device) -> list:
     """Every rank's device as the rank itself sees it (gathered to all ranks): what the line's
     n_gpus / ranks were measured on."""
@@ -641,7 +743,7 @@ def rank_devices(gpu: int, have_gpu: bool, device) -> list:
         uuid = getattr(p, "uuid", None)
         if uuid is not None:
             me["uuid"] = str(uuid)
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _pg():
         return [me]
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, me)
@@ -666,6 +768,12 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: --frames per GPU; strong: --total-frames split over the GPUs")
     ap.add_argument("--total-frames", type=int, default=1 << 23)
+    # auto: a process group only when WORLD_SIZE > 1 (nccl = RCCL; gloo when rehearsing).
+    # nccl / gloo: that backend at every world size, 1 included, so the RCCL init,
+    # all_reduce, all_gather_object, barrier and destroy run on one GPU before any N > 1 run.
+    ap.add_argument("--pg", default=os.environ.get("RXG_BENCH_PG", "auto"), choices=["auto", "nccl", "gloo"])
+    ap.add_argument("--pg-timeout", type=float, default=900.0,
+                    help="seconds any collective may wait (init_process_group timeout)")
     args = ap.parse_args()
     if args.gpus < 1:
         sys.exit(f"bench.py: --gpus {args.gpus}: need at least 1")
@@ -686,11 +794,13 @@ def main():
     rank, world, local = rank_env()
     have_gpu = torch.cuda.device_count() > 0
     gpu = local % max(1, torch.cuda.device_count()) if rehearse else local
-    if world > 1:
+    backend = pg_backend(args.pg, world, rehearse)
+    if backend:
         if have_gpu:
             torch.cuda.set_device(gpu)
-        dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
-    device = torch.device("cpu") if (rehearse and world > 1) or not have_gpu else torch.device("cuda", gpu)
+        init_pg(backend, rank, world, args.pg_timeout)
+    # the collectives' tensors live where the backend reduces them (RCCL: the GPU)
+    device = torch.device("cuda", gpu) if backend == "nccl" or (have_gpu and not backend) else torch.device("cpu")
     ranks = dist.get_world_size() if dist.is_initialized() else 1
     devices = rank_devices(gpu, have_gpu, device)
     if not have_gpu:
@@ -702,8 +812,9 @@ def main():
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "ranks": ranks,
                               "devices": devices, "rehearsal": "no GPU: launcher, rendezvous and collectives only",
+                              "collective_backend": dist.get_backend() if dist.is_initialized() else None,
                               "max_over_ranks_check": t}), flush=True)
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return
     torch.cuda.set_device(gpu)
@@ -790,12 +901,16 @@ def main():
         legs[f"c2_64B_1flow_multiburst_rec{other}"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device,
                                                                      seed, rec=other)
         legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
+        legs["c3_rx_payload_fused"] = fused_leg(eng, wl, args.steps, 2)
+        two = legs["payload_gather"]["kernels_us"] + (region_ms / args.steps * 1e3)
+        legs["c3_rx_payload_fused"]["two_pass_us"] = round(two, 2)  # rx_burst_dev + payload_gather_dev
         legs["tx_generate_dev"] = tx_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)
         legs["c5_bidir_copy_inclusive"] = c5_leg(eng, frames, max(3, args.steps // 4), 1, device,
                                                  seed)
-        if rank == 0:
-            legs["replay_churn"] = replay_churn_leg()
+        if rank == 0:  # bounded: SOLO_BUDGET_S (the others wait at the barrier below)
+            deadline = time.perf_counter() + min(SOLO_BUDGET_S, args.pg_timeout / 3)
+            legs["replay_churn"] = replay_churn_leg(deadline)
             legs["small_burst_latency"] = small_burst_leg(gpu)
         eng.tcb_load(tcb, live)
 
@@ -855,13 +970,14 @@ def main():
             "counters_ok": bool(checks_ok),
             "counters": C,
             "legs": legs,
-            "build": rxg.load_library().rxg_build_info().decode(),
+            **rxg.build_provenance(),  # build (src= hash, rev=), lib, source_hash, build_matches_tree
+            "pg_timeout_s": args.pg_timeout if dist.is_initialized() else None,
         }
         print(json.dumps(line), flush=True)
 
     wl.free()
     eng.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

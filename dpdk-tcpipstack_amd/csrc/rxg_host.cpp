@@ -69,6 +69,7 @@ struct SrvPort {
     unsigned long long done() const;
     bool exited() const;
     void write(unsigned long long q);
+    void cancel(unsigned long long q);
     void request_stop();
     int launch();
     void sync();
@@ -83,7 +84,7 @@ struct rxg_ctx {
     // rxg/librxg_exp.so for scripts/kbench.py and pgbench.py) reads them from the
     // environment; in the product library they stay 0.
     rxg::PackPool pack_pool;  // rxg_rx_burst's packing threads
-    int variant = 0;     // RXG_VARIANT: rx kernel variants (class subsets, ablations)
+    int variant = 0;     // RXG_VARIANT: rx kernel variants (rxg_kernels_exp.hip)
     int nocount = 0;     // RXG_NOCOUNT: skip the counter reduction
     int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather variants
     int mirror_rebuild = 0;  // RXG_MIRROR_REBUILD: every mirror sync a full rebuild (round 1)
@@ -269,15 +270,6 @@ static int ensure(DevBuf &b, size_t bytes)
 
 extern "C" int rxg_abi_version(void) { return RXG_ABI_VERSION; }
 
-extern "C" const char *rxg_build_info(void)
-{
-#ifdef RXG_EXPERIMENTS
-    return "rxg " __DATE__ " gfx950 experiments";
-#else
-    return "rxg " __DATE__ " gfx950";
-#endif
-}
-
 extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
 {
     if (!out) return fail(-EINVAL, "rxg_init: out is NULL");
@@ -367,7 +359,15 @@ extern "C" int rxg_fini(rxg_ctx *c)
 {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
-    (void)rxg_server_stop(c);
+    // A server kernel that missed its time limit may still be resident, reading the tables and
+    // counters and writing the staging and records.  Stop is retried for a bounded time (each
+    // try waits exit_timeout); if the kernel still has not exited, everything it can reach is
+    // deliberately leaked -- the context included -- rather than freed under it: -EIO.
+    int src = rxg_server_stop(c);
+    for (int t = 0; src && t < 4; ++t) src = rxg_server_stop(c);
+    if (src)
+        return fail(-EIO, "rxg_fini: the server kernel has not exited; the context and every buffer it can "
+                          "reach are left allocated (leaked)");
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &r : c->readers)  // table readers still running on caller streams
         if (r.pending && (r.recorded || hipEventRecord(r.e, r.s) == hipSuccess))
@@ -911,11 +911,17 @@ static hipError_t rx_launch(const rxg_ctx *c, const LaunchRx &L, hipStream_t st)
 }
 
 static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
-                         void *stream, const char *who, uint32_t stride64 = 0)
+                         void *stream, const char *who, uint32_t stride64 = 0,
+                         const rxg_payload_slots *pay = nullptr)
 {
+    hipStream_t st = pick(c, stream);
+    // an unregistered stream is refused before anything changes (rxg.h: "-EINVAL, nothing
+    // launched"): no mirror sync, and the previous burst stays replayable
+    if (c->lazy_readers && st != c->stream && !stream_registered(c, st))
+        return fail(-EINVAL, "%s: table-reading launch on stream %p, not registered with rxg_stream_register "
+                             "(RXG_CFG_STREAMS_OUTLIVE_WRITES)", who, (void *)st);
     int rc = begin_bursts(c, frames, bursts, k, rec_kind, who, stride64);
     if (rc) return rc;
-    hipStream_t st = pick(c, stream);
     if ((rc = order_table_reader_before(c, st))) return rc;
     LaunchBurst lb[kMaxBursts];
     for (uint32_t j0 = 0; j0 < k; j0 += kMaxBursts) {
@@ -931,6 +937,10 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
         L.mode = (int)rec_kind;
         L.table = table_view(c);
         L.stride64 = stride64;
+        if (pay) {
+            L.pay_arena = (uint8_t *)pay->arena;
+            L.pay_msgs = pay->msgs;
+        }
         L.counters = c->nocount ? nullptr : c->counters;
         L.max_blocks = c->max_blocks ? c->max_blocks : (rec_kind == RXG_REC48 ? c->grid_rec48
                                                         : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
@@ -939,6 +949,16 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
     }
     if ((rc = order_table_reader_after(c, st))) return rc;
     c->burst_ok = true;
+    if (pay && k == 1 && bursts[0].n) {
+        // rxg_payload_take answers from this burst's messages (fetched at its first call)
+        if (!c->pm_ev) HIP_OK(hipEventCreateWithFlags(&c->pm_ev, hipEventDisableTiming));
+        HIP_OK(hipEventRecord(c->pm_ev, st));
+        c->d_pm = pay->msgs;
+        c->pm_used = nullptr;  // no look-back: never poisoned
+        c->pm_n = bursts[0].n;
+        c->pm_pending = true;
+        c->pm_poisoned = false;
+    }
     return 0;
 }
 
@@ -949,6 +969,17 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
         return fail(-EINVAL, "rxg_rx_burst_dev: NULL device pointer");
     const rxg_dev_burst one{b->off64, b->len, b->n, 0u, b->out};
     return launch_bursts(c, b->frames, &one, 1, b->rec_kind, stream, "rxg_rx_burst_dev");
+}
+
+extern "C" int rxg_rx_burst_payload_dev(rxg_ctx *c, const rxg_dev_batch *b, const rxg_payload_slots *p, void *stream)
+{
+    if (!c || !b || !p) return fail(-EINVAL, "rxg_rx_burst_payload_dev: NULL argument");
+    if (b->n && (!b->frames || !b->off64 || !b->len || !b->out || !p->arena || !p->msgs))
+        return fail(-EINVAL, "rxg_rx_burst_payload_dev: NULL device pointer");
+    if ((uintptr_t)p->arena & 63u) return fail(-EINVAL, "rxg_rx_burst_payload_dev: arena not 64-byte aligned");
+    if ((uintptr_t)p->msgs & 15u) return fail(-EINVAL, "rxg_rx_burst_payload_dev: msgs not 16-byte aligned");
+    const rxg_dev_burst one{b->off64, b->len, b->n, 0u, b->out};
+    return launch_bursts(c, b->frames, &one, 1, b->rec_kind, stream, "rxg_rx_burst_payload_dev", 0u, p);
 }
 
 extern "C" int rxg_rx_bursts_dev(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k,
@@ -1000,6 +1031,9 @@ int SrvPort::launch()
 {
     rxg_ctx::Server &S = c->srv;
     __atomic_store_n(&S.mbox->stop, 0ull, __ATOMIC_RELEASE);  // plain stores: no locked op over the BAR
+    // Load-bearing (rxg_srvfsm.h Port contract): exited reads 0 from here until this launch's
+    // kernel leaves its loop, so the state machine's sync-after-exited never waits on a kernel
+    // that is still resident.  Reset before the launch below, never after it.
     __atomic_store_n(&S.ret->exited, 0ull, __ATOMIC_SEQ_CST);
     _mm_sfence();  // device memory is write-combined on the host
     SrvCtl init;
@@ -1015,13 +1049,6 @@ int SrvPort::launch()
     L.idle_ticks = S.idle_ticks;
     L.blocks = S.blocks;
     L.mode = (int)S.rec_kind;
-#ifdef RXG_EXPERIMENTS
-    L.variant = c->variant;
-    if (c->variant >= 79 && c->variant <= 89) {
-        HIP_OK(launch_server_exp(L, S.st));
-        return 0;
-    }
-#endif
     HIP_OK(launch_server(L, S.st));
     return 0;
 }
@@ -1029,6 +1056,14 @@ int SrvPort::launch()
 unsigned long long SrvPort::done() const { return __atomic_load_n(&c->srv.ret->done, __ATOMIC_ACQUIRE); }
 bool SrvPort::exited() const { return __atomic_load_n(&c->srv.ret->exited, __ATOMIC_ACQUIRE) != 0ull; }
 void SrvPort::sync() { (void)hipStreamSynchronize(c->srv.st); }
+// No kernel is resident (the state machine saw it exit and synchronised its stream): the
+// next kernel starts from `done` (rx_server: last = ret->done, go = done << 16), so setting
+// it to q makes request q, still in the mailbox with a valid check word, one it never serves.
+void SrvPort::cancel(unsigned long long q)
+{
+    __atomic_store_n(&c->srv.ret->done, q, __ATOMIC_SEQ_CST);  // host memory (hipHostMalloc)
+}
+
 void SrvPort::request_stop()
 {
     __atomic_store_n(&c->srv.mbox->stop, 1ull, __ATOMIC_RELEASE);
@@ -1109,7 +1144,8 @@ extern "C" int rxg_server_stop(rxg_ctx *c)
     SrvPort port{c};
     if (c->srv.fsm.stop(port)) {
         // the kernel is still resident and may still write the staging: nothing is freed
-        // (a later stop, or rxg_fini, tries again)
+        // (a later stop tries again; rxg_fini retries a bounded number of times, then leaks
+        // the context and every buffer the kernel can reach)
         return fail(-EIO, "rxg_server_stop: the server kernel has not exited");
     }
     srv_free(c);
@@ -1505,7 +1541,8 @@ extern "C" int rxg_payload_take(rxg_ctx *c, int32_t idx, uint32_t seq, uint32_t 
         uint64_t used = 0;
         HIP_OK(hipMemcpyAsync(c->h_pm, c->d_pm, (size_t)c->pm_n * sizeof(rxg_payload_msg), hipMemcpyDeviceToHost,
                               c->stream));
-        HIP_OK(hipMemcpyAsync(&used, c->pm_used, sizeof used, hipMemcpyDeviceToHost, c->stream));
+        if (c->pm_used)  // (a fused burst, rxg_rx_burst_payload_dev, has no look-back to time out)
+            HIP_OK(hipMemcpyAsync(&used, c->pm_used, sizeof used, hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipStreamSynchronize(c->stream));
         c->pm_pending = false;
         // a gather whose look-back timed out (arena_used = ~0) placed payloads at unknown

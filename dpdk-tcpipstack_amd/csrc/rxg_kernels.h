@@ -29,6 +29,8 @@ struct LaunchRx {
     unsigned long long *counters;
     uint32_t max_blocks;   // grid cap (grid-stride over 64-frame slices)
     uint32_t stride64;     // nonzero: frame i of a burst at slot slot0 + i * stride64 (no off64[])
+    uint8_t *pay_arena;    // non-null (with pay_msgs): the payload hand-off fused in (one burst,
+    rxg_payload_msg *pay_msgs;  //   record kind 8 / 16 / 48; rxg_rx_burst_payload_dev)
     int variant;           // experiment library only (launch_rx_exp): RXG_VARIANT
 };
 
@@ -62,7 +64,7 @@ struct LaunchPayload {
 
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
 #ifdef RXG_EXPERIMENTS
-// rxg_kernels_exp.hip (experiment library only): the ablation kernels of L.variant;
+// rxg_kernels_exp.hip (experiment library only): the experiment kernels of L.variant;
 // hipErrorInvalidValue for a variant it does not know
 hipError_t launch_rx_exp(const LaunchRx &L, hipStream_t st);
 #endif
@@ -152,12 +154,8 @@ struct LaunchServer {
     unsigned long long idle_ticks;  // wall-clock ticks without a request before the kernel exits
     uint32_t blocks;
     int mode;                       // record kind 8 / 16 / 48
-    int variant;                    // experiment library only (launch_server_exp): RXG_VARIANT
 };
 hipError_t launch_server(const LaunchServer &L, hipStream_t st);
-#ifdef RXG_EXPERIMENTS
-hipError_t launch_server_exp(const LaunchServer &L, hipStream_t st);  // rxg_kernels_exp.hip
-#endif
 // rxg_payload.hip: gather of the burst's candidate payloads (one launch + a memset)
 hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *tickets_used);
 uint32_t payload_blocks(uint32_t n);

@@ -155,6 +155,26 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
         return hipGetLastError();
     }
     const bool strided = L.stride64 != 0u;
+    if (L.pay_msgs) {  // the payload hand-off fused in (rxg_rx_burst_payload_dev): one burst
+        if (a.nbursts != 1 || !L.pay_arena) return hipErrorInvalidValue;
+        const dim3 gb(g.blocks), tb(256);
+        switch (L.mode) {
+        case 8:
+            if (strided) hipLaunchKernelGGL((rx_kernel<8, kDescStride, false, false, true>), gb, tb, 0, st, a);
+            else hipLaunchKernelGGL((rx_kernel<8, kDescList, false, false, true>), gb, tb, 0, st, a);
+            break;
+        case 16:
+            if (strided) hipLaunchKernelGGL((rx_kernel<16, kDescStride, false, false, true>), gb, tb, 0, st, a);
+            else hipLaunchKernelGGL((rx_kernel<16, kDescList, false, false, true>), gb, tb, 0, st, a);
+            break;
+        case 48:
+            if (strided) hipLaunchKernelGGL((rx_kernel<48, kDescStride, false, false, true>), gb, tb, 0, st, a);
+            else hipLaunchKernelGGL((rx_kernel<48, kDescList, false, false, true>), gb, tb, 0, st, a);
+            break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (L.mode) {
     case 8: strided ? launch_mode<8, kDescStride>(a, g, st) : launch_mode<8, kDescList>(a, g, st); break;
     case 16: strided ? launch_mode<16, kDescStride>(a, g, st) : launch_mode<16, kDescList>(a, g, st); break;

@@ -111,6 +111,11 @@ struct RxArgs {
     DevTable t;
     unsigned long long *counters;
     RxBurst b[kMaxBursts];
+    // PAY kernels (rxg_rx_burst_payload_dev, one burst): the payload hand-off fused into the
+    // pass over the frames -- payload lines to pay_arena (the frame pool's geometry), one
+    // rxg_payload_msg per frame to pay_msgs.  (Last: the other fields keep their offsets.)
+    uint8_t *pay_arena;
+    rxg_payload_msg *pay_msgs;
 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -211,6 +216,62 @@ struct Rec {
     uint4 q0, q1, q2;
 };
 
+// ------------------------------------------------- fused payload hand-off (PAY) ---
+// The payload a frame hands to the socket ring (the candidates of
+// rxg_payload_gather_dev, oracle/payload.py): a TCP segment (ether_type IPv4, proto 6: the
+// verdicts DISPATCH / RST_NOPCB / RST_LISTEN_NONSYN) of at least 54 bytes, datalen =
+// total_length - IHL*4 - data_off*4 > 0 (tcp_states.c:103-111), whose Length = datalen bytes
+// at frame + 34 + data_off*4 (GetData takes the IP header as 20 bytes, tcp_windows.c:164-166)
+// lie inside the frame.  et / tlw packed as Fields::et / Fields::tl.  Returns start << 16 |
+// datalen (a candidate's datalen fits 16 bits: it lies inside the frame), or 0.
+__device__ __forceinline__ uint32_t pay_span(bool valid, uint32_t len, uint32_t et, uint32_t tlw)
+{
+    const uint32_t tl = tlw & 0xFFFFu, vihl = (tlw >> 16) & 0xFFu, doff = tlw >> 24;
+    const int32_t datalen = (int32_t)tl - (int32_t)(vihl & 0xFu) * 4 - (int32_t)(doff >> 4) * 4;
+    const uint32_t start = RXG_OFF_TCP + (doff >> 4) * 4u;
+    const bool cand = valid && (et & 0xFFFFu) == RXG_ETHER_TYPE_IPV4 && ((et >> 16) & 0xFFu) == RXG_IPPROTO_TCP &&
+                      len >= 54u && datalen > 0 && start + (uint32_t)datalen <= len;
+    return cand ? (start << 16) | (uint32_t)datalen : 0u;
+}
+
+__device__ __forceinline__ void nt_store16(uint8_t *p, const uint32_t (&q)[4])
+{
+    u32x4 v;
+    v.x = q[0]; v.y = q[1]; v.z = q[2]; v.w = q[3];
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+}
+
+// The 64-byte lines of a frame that hold its payload: [lo, hi].
+__device__ __forceinline__ void pay_lines_of(uint32_t span, uint32_t &lo, uint32_t &hi)
+{
+    const uint32_t start = span >> 16, end = start + (span & 0xFFFFu);
+    lo = start >> 6;
+    hi = (end - 1u) >> 6;
+}
+
+// The frame's message (rxg_payload_msg): the payload at arena + 64*off + start, in place of
+// the frame's own bytes (the arena has the pool's geometry), or zeros.  f: its index in the
+// burst.  One 16-byte non-temporal store per lane.
+__device__ __forceinline__ void pay_msg(const RxArgs &a, uint32_t f, bool valid, uint32_t off, uint32_t span)
+{
+    if (!valid) return;
+    const uint32_t dl = span & 0xFFFFu;
+    const uint64_t ao = span ? (uint64_t)off * 64u + (span >> 16) : 0ull;
+    const uint32_t q[4] = {(uint32_t)ao, (uint32_t)(ao >> 32), dl,
+                           span ? (RXG_PM_GATHERED | (dl >= 1000u ? RXG_PM_REF_OVERSIZE : 0u)) : 0u};
+    nt_store16(reinterpret_cast<uint8_t *>(a.pay_msgs + f), q);
+}
+
+// A frame of <= 64 bytes owned by one lane (the all-small path after its transpose): its one
+// line, as loaded, when it carries a payload.
+__device__ __forceinline__ void pay_line_small(const RxArgs &a, uint32_t off, uint32_t span, const uint32_t (&q)[4][4])
+{
+    if (span == 0u) return;
+    uint8_t *dst = a.pay_arena + (size_t)off * 64u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nt_store16(dst + 16 * k, q[k]);
+}
+
 // ------------------------------------------------------------- one round of frames ---
 //
 // Phase A (streaming): the lanes of a group load one frame, sum it and extract its header.
@@ -288,21 +349,23 @@ __device__ __forceinline__ void load_chunks(const RxArgs &a, uint32_t off, uint3
     }
 }
 
-template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PAY = false>
 __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                int lane, uint32_t (&d)[NLOAD][4]);
 
-template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PAY = false>
 __device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                               int lane)
 {
     uint32_t d[NLOAD][4];
     load_chunks<LPF, NLOAD, NT>(a, off, len, active, lane, d);
-    return frame_fields<LPF, NLOAD, JUMBO, MODE, NT>(a, off, len, active, lane, d);
+    return frame_fields<LPF, NLOAD, JUMBO, MODE, NT, PAY>(a, off, len, active, lane, d);
 }
 
-// Sums, header fields and (TX) checksum stores of the frames whose chunks are in d.
-template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT>
+// Sums, header fields and (TX) checksum stores of the frames whose chunks are in d; PAY (the
+// jumbo class, frames over 2 KiB): the payload lines copied by the group, loaded again (the
+// chunks in d are only the first LPF * NLOAD).
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PAY>
 __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                int lane, uint32_t (&d)[NLOAD][4])
 {
@@ -406,6 +469,19 @@ __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, ui
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
+    if constexpr (PAY) {  // every lane holds the header here (hdr_dword)
+        const uint32_t span = pay_span(active, len, F.et, F.tl);
+        if (span != 0u) {
+            uint32_t lo, hi;
+            pay_lines_of(span, lo, hi);
+            uint8_t *dst = a.pay_arena + (size_t)off * 64u;
+            for (uint32_t c = 4u * lo + (uint32_t)gl; c < 4u * (hi + 1u); c += (uint32_t)LPF) {
+                const uint4 v = load16<NT>(fp + 16u * c);
+                const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+                nt_store16(dst + 16u * c, q);
+            }
+        }
+    }
     if constexpr (TX) {
         // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118); bytes at or
         // beyond data_len are never written
@@ -569,14 +645,16 @@ __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32
 // The loads of one round of a streaming class: lane l of a group of LPF loads chunks
 // l, l + LPF, ... of its frame.  Inactive lanes: off = len = 0 (the arena's first SAFE bytes
 // exist: it holds a frame of this class).
-template <int C, int LPF, int NLOAD, bool NT>
+template <int C, int LPF, int NLOAD, bool NT, bool PAY = false>
 __device__ __forceinline__ void round_load(const RxArgs &a, uint32_t off, uint32_t len, int lane,
                                            uint32_t (&d)[NLOAD][4])
 {
     constexpr int SAFE = (class_min_len(C) + 63) & ~63;  // bytes every frame of the class has
     const int gl = lane & (LPF - 1);
     const uint8_t *fp = a.frames + (size_t)off * 64u;
-    const uint32_t lastc = len ? ((len - 1u) & ~15u) : 0u;
+    // PAY: chunks up to the end of the frame's last 64-byte line are loaded as they are (that
+    // line is readable, rxg_dev_batch): the payload's lines are written whole
+    const uint32_t lastc = len ? (PAY ? ((len + 63u) & ~63u) - 16u : ((len - 1u) & ~15u)) : 0u;
 #pragma unroll
     for (int j = 0; j < NLOAD; ++j) {
         const uint32_t o = (uint32_t)(gl + j * LPF) * 16u;
@@ -589,21 +667,22 @@ __device__ __forceinline__ void round_load(const RxArgs &a, uint32_t off, uint32
     }
 }
 
-template <int C, int LPF, int NLOAD, int MODE, bool NT>
+template <int C, int LPF, int NLOAD, int MODE, bool NT, bool PAY = false>
 __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                       int lane, uint32_t (&d)[NLOAD][4]);
 
-template <int C, int LPF, int NLOAD, int MODE, bool NT>
+template <int C, int LPF, int NLOAD, int MODE, bool NT, bool PAY = false>
 __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                    int lane)
 {
     uint32_t d[NLOAD][4];
-    round_load<C, LPF, NLOAD, NT>(a, off, len, lane, d);
-    return frame_round_compute<C, LPF, NLOAD, MODE, NT>(a, off, len, active, lane, d);
+    round_load<C, LPF, NLOAD, NT, PAY>(a, off, len, lane, d);
+    return frame_round_compute<C, LPF, NLOAD, MODE, NT, PAY>(a, off, len, active, lane, d);
 }
 
-// Sums, header fields and (tx) checksum stores of one round whose chunks are in d.
-template <int C, int LPF, int NLOAD, int MODE, bool NT>
+// Sums, header fields and (tx) checksum stores of one round whose chunks are in d; PAY: the
+// payload lines written to the arena from the same registers.
+template <int C, int LPF, int NLOAD, int MODE, bool NT, bool PAY>
 __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                       int lane, uint32_t (&d)[NLOAD][4])
 {
@@ -697,6 +776,23 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
+    if constexpr (PAY) {
+        // The payload hand-off fused in: the leader's header gives the span (pay_span); every
+        // lane of the group writes those of its chunks that fall in the payload's 64-byte
+        // lines, as loaded, at the same offset in the arena.  Whole lines (no partial-line
+        // writes), no byte shift; the bytes written are the pool's own.
+        const uint32_t span = lane_read(pay_span(leader, len, F.et, F.tl), gbase);
+        if (active && span != 0u) {
+            uint32_t lo, hi;
+            pay_lines_of(span, lo, hi);
+            uint8_t *dst = a.pay_arena + (size_t)off * 64u;
+#pragma unroll
+            for (int j = 0; j < NLOAD; ++j) {
+                const uint32_t c = (uint32_t)(gl + j * LPF), line = c >> 2;
+                if (line >= lo && line <= hi) nt_store16(dst + 16u * c, d[j]);
+            }
+        }
+    }
     if constexpr (TX) {
         // ip_out stores both as htons(calculate_checksum(...)) (ip.c:107,118).  Frames of
         // these classes are longer than 64 bytes: the group writes the frame's whole first
@@ -726,7 +822,7 @@ __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int l
 
 // part / parts: this wave takes rounds part, part + parts, ... of the class (the server's
 // cooperative single slice, rx_body; 0 / 1 everywhere else).
-template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PIPE = false>
+template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PIPE = false, bool PAY = false>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
                                           int lane_in, uint32_t *sf, uint32_t part = 0u, uint32_t parts = 1u)
 {
@@ -755,6 +851,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
     // of a load in flight).  Loads are issued unconditionally, a round past the class's last
     // frame reading the arena's first bytes with every lane inactive: a load under a branch
     // leaves the wait at the join counting as if it were absent (vmcnt(0)).  DESIGN.md §5.
+    static_assert(!(PIPE && PAY), "the pipelined rounds (tx, server) carry no payload hand-off");
     if constexpr (PIPE && LPF >= 2 && !JUMBO) {
         uint32_t dA[NLOAD][4], dB[NLOAD][4];
         auto rmeta = [&](uint32_t r, uint32_t &korig, uint32_t &koff, uint32_t &klen) -> bool {
@@ -829,10 +926,11 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             // (MODE 0, tx: no parked fields; the transpose uses the 4 KiB ring area itself)
             transpose_small_slice(v, rl, sf + (MODE == 0 ? 0 : MODE == 48 ? NF48 * 64 : NF16 * 64), d);
             F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
+            if constexpr (PAY) pay_line_small(a, koff, pay_span(act, klen, F.et, F.tl), d);
         } else if constexpr (LPF >= 2 && !JUMBO)
-            F = frame_round_fast<C, LPF, NLOAD, MODE, NT>(a, act ? koff : 0u, act ? klen : 0u, act, rl);
+            F = frame_round_fast<C, LPF, NLOAD, MODE, NT, PAY>(a, act ? koff : 0u, act ? klen : 0u, act, rl);
         else
-            F = frame_round<LPF, NLOAD, JUMBO, MODE, NT>(a, koff, act ? klen : 0u, act, rl);
+            F = frame_round<LPF, NLOAD, JUMBO, MODE, NT, PAY>(a, koff, act ? klen : 0u, act, rl);
         if constexpr (MODE != 0) {
             if (act && (lane & (LPF - 1)) == 0) park_fields<MODE>(sf, korig, F);
         }
@@ -841,23 +939,6 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
 
 // Phase B: lane i classifies frame i of the slice (all 64 probes in flight together) and
 // writes its record; the records of a slice are one contiguous 1 KiB / 3 KiB store.
-// ABL (ablation bits, experiment builds only: where a kernel's time goes, timing only):
-constexpr int kAblNoProbe = 1;      // no TCB / ARP probe: every frame misses
-constexpr int kAblNoStore = 2;      // no record stores
-constexpr int kAblNoPhaseB = 4;     // no classify at all (parse + checksums only)
-constexpr int kAblHotBuckets = 8;   // every probe reads one of the first 256 buckets (cache-resident)
-constexpr int kAblNoSearch = 16;    // the first bucket's first slot taken as the hit: loads without the search
-constexpr int kAblStamps = 32;      // (server, one slice) lane 0 stamps the all-small step's phases
-                                    // into the words at RxArgs::sel (rx_server SRVX 256)
-template <int ABL>
-__device__ __forceinline__ void abl_stamp(const RxArgs &a, int lane, int k)
-{
-    if constexpr ((ABL & kAblStamps) != 0) {
-        const unsigned long long t = (unsigned long long)wall_clock64();
-        if (lane == 0 && (threadIdx.x >> 6) == 0)
-            reinterpret_cast<unsigned long long *>(const_cast<uint32_t *>(a.sel))[k] = t;
-    }
-}
 // First bucket of the exact-tuple probe, loaded early so that several frames' probes of
 // one lane are in flight together.
 struct Probe {
@@ -877,12 +958,10 @@ __device__ __forceinline__ uint4 arp_issue(const RxArgs &a, const Fields &F)
     return a.t.arp[b];
 }
 
-template <int ABL = 0>
 __device__ __forceinline__ Probe probe_issue(const RxArgs &a, const Fields &F)
 {
     Probe P;
     P.hb = tuple_hash(F.ports, F.dst, bswap32(F.src)) & a.t.bucket_mask;
-    if constexpr ((ABL & kAblHotBuckets) != 0) P.hb &= 255u;
     // always a valid bucket: load unconditionally (see load_chunks), use only for TCP
     const uint4 *b = a.t.buckets + (size_t)P.hb * kSlotsPerBucket;
 #pragma unroll
@@ -913,7 +992,7 @@ __device__ __forceinline__ Probe probe_none()
     return P;
 }
 
-template <int MODE, bool VWALK, int ABL>
+template <int MODE, bool VWALK>
 __device__ __forceinline__ void classify_finish(const RxArgs &a, bool valid, uint32_t len, const Fields &F,
                                                 const Probe &P, WaveCounters &wc, Rec &pr, FlowCache &fc,
                                                 bool cached);
@@ -944,13 +1023,11 @@ struct ProbeLoads {
     uint32_t hb;           // this lane's frame's first bucket
 };
 
-template <int ABL = 0>
 __device__ __forceinline__ ProbeLoads probe_issue_coalesced(const RxArgs &a, const Fields &F, int lane)
 {
     static_assert(kSlotsPerBucket == 4, "one bucket = four 16-byte slots = four lanes");
     ProbeLoads L;
     L.hb = probe_bucket(a, F);
-    if constexpr ((ABL & kAblHotBuckets) != 0) L.hb &= 255u;
     const uint4 *bk = a.t.buckets + (lane & 3);
     const uint32_t h0 = lane_read(L.hb, (lane >> 2)), h1 = lane_read(L.hb, 16 + (lane >> 2));
     const uint32_t h2 = lane_read(L.hb, 32 + (lane >> 2)), h3 = lane_read(L.hb, 48 + (lane >> 2));
@@ -987,7 +1064,7 @@ __device__ __forceinline__ Probe probe_transpose(const ProbeLoads &L, int lane, 
 
 // Classify lane's frame and leave its record in pr.  tsf: 4 KiB of LDS for the probe's
 // transpose.
-template <int MODE, bool VWALK, int ABL>
+template <int MODE, bool VWALK>
 __device__ __forceinline__ void classify_store(const RxArgs &a, bool valid, uint32_t len, const Fields &F,
                                                WaveCounters &wc, Rec &pr, FlowCache &fc, uint32_t *tsf)
 {
@@ -995,9 +1072,8 @@ __device__ __forceinline__ void classify_store(const RxArgs &a, bool valid, uint
     const bool is_tcp = valid && et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
     const int lane = (int)(threadIdx.x & 63);
-    const Probe P = (cached || (ABL & kAblNoProbe)) ? probe_none()
-                                                    : probe_transpose(probe_issue_coalesced<ABL>(a, F, lane), lane, tsf);
-    classify_finish<MODE, VWALK, ABL>(a, valid, len, F, P, wc, pr, fc, cached);
+    const Probe P = cached ? probe_none() : probe_transpose(probe_issue_coalesced(a, F, lane), lane, tsf);
+    classify_finish<MODE, VWALK>(a, valid, len, F, P, wc, pr, fc, cached);
 }
 
 // Overflow walks (a tuple or an ARP address not in its first bucket, which was loaded with
@@ -1124,7 +1200,7 @@ __device__ __forceinline__ uint32_t tuple_lookup(const RxArgs &a, const Probe &P
     return v;
 }
 
-template <int MODE, bool VWALK, int ABL>
+template <int MODE, bool VWALK>
 __device__ __forceinline__ void classify_finish(const RxArgs &a, bool valid, uint32_t len, const Fields &F,
                                                 const Probe &P, WaveCounters &wc, Rec &pr, FlowCache &fc,
                                                 bool cached)
@@ -1164,8 +1240,8 @@ __device__ __forceinline__ void classify_finish(const RxArgs &a, bool valid, uin
             nslot = (fc.meta >> 9) & 1u;
             arp_learn = (fc.meta >> 10) & 1u;
         }
-    } else if (is_tcp && !(ABL & kAblNoProbe)) {
-        const uint32_t v = (ABL & kAblNoSearch) ? P.s[0].w : tuple_lookup<VWALK>(a, P, ports, dst_raw, src_host);
+    } else if (is_tcp) {
+        const uint32_t v = tuple_lookup<VWALK>(a, P, ports, dst_raw, src_host);
         if (v != kEmpty) {
             idx = (int32_t)(v & kIdxMask);
             st = v >> kStateShift;
@@ -1429,7 +1505,7 @@ struct RecRing {
 
 // One all-small slice s whose frames are in flight in vb[P]; prefetches slice s + nwaves
 // into vb[1-P] when it is all-small too (and returns true: the caller continues the run).
-template <int P, int MODE, int DESC, bool VWALK, int ABL, int RS, typename BC>
+template <int P, int MODE, int DESC, bool VWALK, int RS, bool PAY, typename BC>
 __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &s, uint32_t nslices,
                                            uint32_t nwaves, uint32_t &c_off, uint32_t &c_len, uint32_t &n_off,
                                            uint32_t &n_len, uint4 (&vb)[2][4], RecRing<MODE, RS> &ring,
@@ -1446,14 +1522,17 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     const bool valid = !VWALK || (uint32_t)lane < slice_frames(a, uniform(s), bc);
     uint32_t d[4][4];
     uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
-    abl_stamp<ABL>(a, lane, 0);
     transpose_small_slice(vb[P], lane, sf, d);
-    abl_stamp<ABL>(a, lane, 1);
     // the next slice's descriptors are read after this slice's frames have landed: they were
     // issued before them (loop top) or just after (previous step), so this waits for no
     // more than the frames did
     const bool nxt = s1 < nslices && slice_frames(a, uniform(s1), bc) == 64u && __ballot(n_len <= 64u) == ~0ull;
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
+    if constexpr (PAY) {  // (one burst per PAY launch: frame s * 64 + lane)
+        const uint32_t span = pay_span(valid, c_len, F.et, F.tl);
+        pay_line_small(a, c_off, span, d);
+        pay_msg(a, s * 64u + (uint32_t)lane, valid, c_off, span);
+    }
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
@@ -1461,8 +1540,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     // frames' LDS (as the class path does) measured 64 B at 64 K flows 28.8 -> 25.9 us, but
     // the one-flow C2 burst, which never probes, 19.2 -> 20.6 (more registers live across
     // the prefetch); the C2 configuration is the one the metric names.
-    abl_stamp<ABL>(a, lane, 2);
-    const Probe PO = ((ABL & kAblNoProbe) || cached) ? probe_none() : probe_issue<ABL>(a, F);
+    const Probe PO = cached ? probe_none() : probe_issue(a, F);
     // The next slice's frames are issued whether or not the run continues (a run's last step
     // reads the arena's first bytes instead): the compiler cannot count a load issued under a
     // branch, and the probe's wait below then drained the prefetch too (64 B frames at 64 K
@@ -1470,15 +1548,10 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     issue_small_slice<true>(a, nxt ? n_off : 0u, nxt ? n_len : 0u, lane, vb[1 - P]);
     uint32_t y_off, y_len;
     load_desc<DESC>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
-    abl_stamp<ABL>(a, lane, 3);
-    classify_finish<MODE, VWALK, ABL>(a, valid, c_len, F, PO, wc, rec, fc, cached);
-    abl_stamp<ABL>(a, lane, 4);
+    classify_finish<MODE, VWALK>(a, valid, c_len, F, PO, wc, rec, fc, cached);
     bytes += valid ? c_len : 0u;
-    if (!(ABL & kAblNoStore)) {
-        if (ring.n == RS) ring.template flush<true>(a, lane, bc);
-        ring.put(s, lane, rec);
-    }
-    abl_stamp<ABL>(a, lane, 5);
+    if (ring.n == RS) ring.template flush<true>(a, lane, bc);
+    ring.put(s, lane, rec);
     s = s1;
     c_off = n_off; c_len = n_len;
     n_off = y_off; n_len = y_len;
@@ -1492,7 +1565,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
 // ahead and are issued before the frames (vmcnt retires in order: the next step's check of
 // them then waits for nothing younger).  pend: s + nwaves's frames are in vb[1-P]; returns
 // whether the run continues with it.
-template <int P, int MODE, int DESC, bool VWALK, int ABL, int RS, typename BC>
+template <int P, int MODE, int DESC, bool VWALK, int RS, bool PAY, typename BC>
 __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t &s, uint32_t nslices,
                                             uint32_t nwaves, uint32_t &c_off, uint32_t &c_len, uint32_t &n_off,
                                             uint32_t &n_len, uint32_t &y_off, uint32_t &y_len, bool &pend,
@@ -1504,20 +1577,23 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
     uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
     transpose_small_slice(vb[P], lane, sf, d);
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
+    if constexpr (PAY) {
+        const uint32_t span = pay_span(true, c_len, F.et, F.tl);
+        pay_line_small(a, c_off, span, d);
+        pay_msg(a, s * 64u + (uint32_t)lane, true, c_off, span);
+    }
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
     const bool cached = __ballot(is_tcp && !fc_hit(fc, F)) == 0ull;
-    const Probe PO = ((ABL & kAblNoProbe) || cached) ? probe_none() : probe_issue<ABL>(a, F);
+    const Probe PO = cached ? probe_none() : probe_issue(a, F);
     uint32_t z_off, z_len;
     load_desc<DESC>(a, s + 3u * nwaves, lane, z_off, z_len, bc);
     const bool nxt2 = pend && s2 < nslices && slice_frames(a, uniform(s2), bc) == 64u && __ballot(y_len <= 64u) == ~0ull;
     issue_small_slice<true>(a, nxt2 ? y_off : 0u, nxt2 ? y_len : 0u, lane, vb[P]);  // unconditional, as in small_step
-    classify_finish<MODE, VWALK, ABL>(a, true, c_len, F, PO, wc, rec, fc, cached);
+    classify_finish<MODE, VWALK>(a, true, c_len, F, PO, wc, rec, fc, cached);
     bytes += c_len;
-    if (!(ABL & kAblNoStore)) {
-        if (ring.n == RS) ring.template flush<true>(a, lane, bc);
-        ring.put(s, lane, rec);
-    }
+    if (ring.n == RS) ring.template flush<true>(a, lane, bc);
+    ring.put(s, lane, rec);
     const bool cont = pend;
     pend = nxt2;
     s = s1;
@@ -1535,11 +1611,11 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
 //   MULTI  several bursts of one frame pool per launch (BurstCursor)
 //   DEEP   runs of all-small slices prefetched two slices deep (small_step2); launch_rx picks
 //          it for launches of at least kDeepSlicesPerWave slices per wave
+//   PAY    the payload hand-off fused in (rxg_rx_burst_payload_dev: one burst, launched)
 //   SRV    the server's form: streaming-class rounds software-pipelined (a served burst's
 //          frame reads are latency-bound: 32 x 1500 B bursts 25.6-27.6 -> 22.2-23.2 us) and
 //          overflow walks with vector loads (VWALK, see sload_bucket)
-//   ABL    ablation bits (experiment library only; 0 in every product kernel)
-template <int MODE, int DESC, bool MULTI, bool DEEP, bool SRV, int ABL>
+template <int MODE, int DESC, bool MULTI, bool DEEP, bool SRV, bool PAY = false>
 __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
 {
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -1577,7 +1653,6 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     BurstCursor<MULTI> bc;
     bc.load(a, lane);
     const uint32_t nslices = a.nslices;
-    abl_stamp<ABL>(a, lane, 8);
     // The streaming classes' rounds software-pipelined in tx (MODE 0, 101
     // VGPRs) and in the server; in launched rx, at the occupancy grid, the second buffer's
     // register cap cost more than the overlap gained.  Multi-burst kernels keep the plain
@@ -1644,7 +1719,6 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
             // (the server: a partial slice whose valid frames are all small too -- a served
             // burst of fewer than 64 frames is one; its invalid lanes classify nothing)
             const bool all_small = __ballot(cls == 0 || (SRV && !valid)) == ~0ull;
-            abl_stamp<ABL>(a, lane, 9);
             if (all_small) {
                 // A run of all-small slices (every frame <= 64 bytes; lane i owns frame i end
                 // to end), prefetched one slice deep: the next slice's frame loads are issued
@@ -1655,7 +1729,6 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
                 // register copy of a load in flight would wait for it).
                 uint4 vb[2][4];
                 issue_small_slice<true>(a, c_off, c_len, lane, vb[0]);
-                abl_stamp<ABL>(a, lane, 10);
                 if constexpr (DEEP) {
                     // two-deep: s + nwaves's frames too when that slice is all-small
                     const uint32_t s1 = s + nwaves;
@@ -1664,11 +1737,11 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
                     load_desc<DESC>(a, s + 2u * nwaves, lane, y_off, y_len, bc);
                     if (pend) issue_small_slice<true>(a, n_off, n_len, lane, vb[1]);
                     for (;;) {
-                        if (!small_step2<0, MODE, DESC, SRV, ABL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
+                        if (!small_step2<0, MODE, DESC, SRV, RS, PAY>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
                                                                       n_len, y_off, y_len, pend, vb, ring, wc, rec,
                                                                       fcache, bytes, bc))
                             break;
-                        if (!small_step2<1, MODE, DESC, SRV, ABL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
+                        if (!small_step2<1, MODE, DESC, SRV, RS, PAY>(a, lane, s, nslices, nwaves, c_off, c_len, n_off,
                                                                       n_len, y_off, y_len, pend, vb, ring, wc, rec,
                                                                       fcache, bytes, bc))
                             break;
@@ -1676,10 +1749,10 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
                     continue;
                 }
                 for (;;) {
-                    if (!small_step<0, MODE, DESC, SRV, ABL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off, n_len,
+                    if (!small_step<0, MODE, DESC, SRV, RS, PAY>(a, lane, s, nslices, nwaves, c_off, c_len, n_off, n_len,
                                                                  vb, ring, wc, rec, fcache, bytes, bc))
                         break;
-                    if (!small_step<1, MODE, DESC, SRV, ABL, RS>(a, lane, s, nslices, nwaves, c_off, c_len, n_off, n_len,
+                    if (!small_step<1, MODE, DESC, SRV, RS, PAY>(a, lane, s, nslices, nwaves, c_off, c_len, n_off, n_len,
                                                                  vb, ring, wc, rec, fcache, bytes, bc))
                         break;
                 }
@@ -1702,42 +1775,38 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         const uint32_t parts = coop ? 4u / ck : 1u;
         // classes 0-2 of mixed slices: plain loads; the larger ones non-temporal (measured
         // +5 % at 1500 B, -4 % at 64 B)
-        run_class<0, 1, 4, false, MODE, false>(a, cls, off, len, lane, sf);
-        run_class<1, 2, 4, false, MODE, false, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<2, 4, 4, false, MODE, false, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<3, 8, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<10, 8, 5, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<8, 8, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<4, 16, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<5, 16, 6, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<6, 32, 4, false, MODE, true, PIPE>(a, cls, off, len, lane, sf, 0u, parts);
-        run_class<7, 64, 2, true, MODE, true>(a, cls, off, len, lane, sf, 0u, parts);
-        abl_stamp<ABL>(a, lane, 12);
+        run_class<0, 1, 4, false, MODE, false, false, PAY>(a, cls, off, len, lane, sf);
+        run_class<1, 2, 4, false, MODE, false, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<2, 4, 4, false, MODE, false, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<3, 8, 4, false, MODE, true, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<10, 8, 5, false, MODE, true, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<8, 8, 6, false, MODE, true, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<4, 16, 4, false, MODE, true, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<5, 16, 6, false, MODE, true, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<6, 32, 4, false, MODE, true, PIPE, PAY>(a, cls, off, len, lane, sf, 0u, parts);
+        run_class<7, 64, 2, true, MODE, true, false, PAY>(a, cls, off, len, lane, sf, 0u, parts);
         if constexpr (SRV && MODE != 0) {
             if (coop) __syncthreads();  // the other waves' parked fields
         }
-        abl_stamp<ABL>(a, lane, 13);
-        if constexpr (MODE == 0 || (ABL & kAblNoPhaseB)) {
+        if constexpr (MODE == 0) {
             wcount(wc, RXG_C_RX, valid);
         } else {
             // the fields parked by other lanes of this wave must be visible to this lane
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            classify_store<MODE, SRV, ABL>(a, valid, len, unpark_fields<MODE>(sf, lane), wc, rec, fcache, sf + NF * 64);
-            abl_stamp<ABL>(a, lane, 14);
+            const Fields F = unpark_fields<MODE>(sf, lane);
+            if constexpr (PAY) pay_msg(a, s * 64u + (uint32_t)lane, valid, off, pay_span(valid, len, F.et, F.tl));
+            classify_store<MODE, SRV>(a, valid, len, F, wc, rec, fcache, sf + NF * 64);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
-            if (!(ABL & kAblNoStore)) {
-                if (ring.n == RS) ring.flush(a, lane, bc);
-                ring.put(s, lane, rec);
-            }
+            if (ring.n == RS) ring.flush(a, lane, bc);
+            ring.put(s, lane, rec);
         }
         s += nwaves;
         c_off = n_off; c_len = n_len;
         n_off = y_off; n_len = y_len;
     }
     if constexpr (MODE != 0) ring.flush(a, lane, bc);
-    abl_stamp<ABL>(a, lane, 6);
 
     if (a.counters == nullptr) return;
     if constexpr (SRV) {
@@ -1759,7 +1828,6 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         for (int k = 0; k < RXG_NCOUNTERS; ++k) mine = lane == k ? wc.c[k] : mine;
         const unsigned long long v = (MODE != 0 && lane == RXG_C_BYTES) ? tot : (unsigned long long)mine;
         if (lane < RXG_NCOUNTERS && v) atomicAdd(&a.counters[(blk % kKernelCounterRows) * RXG_NCOUNTERS + lane], v);
-        abl_stamp<ABL>(a, lane, 7);
         return;
     }
     // wave -> workgroup -> one atomic per counter
@@ -1780,15 +1848,15 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
         // replica row per workgroup (rxg.h RXG_COUNTER_ROWS): 32 adders per line, not 2048
         if (v) atomicAdd(&a.counters[(blk % kKernelCounterRows) * RXG_NCOUNTERS + k], v);
     }
-    abl_stamp<ABL>(a, lane, 7);
 }
 
 // One launch per batch (rxg_rx_burst_dev / _bursts_dev / _strided_dev, the replay's
 // re-classification, rxg_tx_cksum_dev): a grid-stride over the launch's slices.
-template <int MODE, int DESC, bool MULTI, bool DEEP, int ABL = 0>
+template <int MODE, int DESC, bool MULTI, bool DEEP, bool PAY = false>
 __global__ __launch_bounds__(256, 1) void rx_kernel(RxArgs a)
 {
-    rx_body<MODE, DESC, MULTI, DEEP, false, ABL>(a, blockIdx.x, gridDim.x);
+    static_assert(!(PAY && (MULTI || MODE == 0 || DESC == kDescSel)), "PAY: one receive burst");
+    rx_body<MODE, DESC, MULTI, DEEP, false, PAY>(a, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------- latency-mode server ---
@@ -1841,18 +1909,8 @@ __device__ __forceinline__ uint32_t row_xor16(uint32_t v)
     return v;
 }
 
-// SRVX (experiment builds, timing only: where a served burst's microseconds go): 1 = no rx
-// body (the protocol alone), 2 = no acquire at the request, 4 = no release before `done`,
-// 8 = workgroup 0's thread 0 stamps each request's phases (constant-rate wall clock and the
-// shader clock) into the counters block past its first row (which a one-workgroup server
-// counts in): 8 words per request at 16 + (number mod 32) * 8 -- seen, acquired, body done,
-// stores landed, released, and the shader clock at acquired / released; 16 / 32 / 64 / 128
-// with 8: the body without its TCB probe / its record stores / with cache-resident buckets /
-// without the search (kAblNoProbe / kAblNoStore / kAblHotBuckets / kAblNoSearch); 256 with
-// 8: the body's own phases too (kAblStamps: 16 more words per request after the 32 above);
-// 512 with 8: the body run twice per request, the second end stamped in word 7.
 // Three waves per SIMD at most (168 VGPRs): the pipelined rounds would otherwise take 170.
-template <int MODE, int SRVX = 0>
+template <int MODE>
 __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
 {
     __shared__ SrvReq s_req;
@@ -1864,7 +1922,6 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
     // take part in was published, still sees g as new, since g is not done without it.
     unsigned long long last = 0ull;
     if (threadIdx.x == 0) last = __hip_atomic_load(&sa.ret->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    unsigned long long stamp[8] = {};  // SRVX & 8 (thread 0 of workgroup 0)
     for (;;) {
         if (blockIdx.x == 0 && threadIdx.x < 64) {
             // wave 0 polls the mailbox's first 320 bytes (lane l < 40: bytes 8l .. 8l+7) in
@@ -1874,9 +1931,7 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
             const unsigned long long lst = __shfl(last, 0, 64);
             const long long t0 = wall_clock64();
             unsigned long long q;
-            uint32_t polls = 0u;  // (SRVX & 256: the poll loop's iterations, stamped)
             for (;;) {
-                if constexpr ((SRVX & 256) != 0) ++polls;
                 unsigned long long w = 0ull;
                 if (l < kSrvPollWords)
                     w = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(sa.mbox) + l, __ATOMIC_RELAXED,
@@ -1921,20 +1976,8 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
             // (mirror tables, caller frames); waited for before any wave of the workgroup loads
             // (MI355X_MICROARCH.md, inter-workgroup visibility).  A first form with relaxed
             // polls and no acquire served stale staging lines (test_gpu_server).
-            if constexpr ((SRVX & 8) != 0) stamp[0] = (unsigned long long)wall_clock64();
-            if constexpr ((SRVX & 256) != 0) {
-                if (l == 0 && q != kSrvStop) {  // the poll loop's start and iterations
-                    unsigned long long *d = sa.counters + 16u + 32u * 8u + (q & 31u) * 16u;
-                    d[12] = (unsigned long long)t0;
-                    d[13] = polls;
-                }
-            }
-            if constexpr (!(SRVX & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr ((SRVX & 8) != 0) {
-                stamp[1] = (unsigned long long)wall_clock64();
-                stamp[5] = __builtin_amdgcn_s_memtime();
-            }
             // the request's words, written by lanes 1-11, for lane 0
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -2010,19 +2053,7 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
         a.b[0].n = uniform(s_req.n);
         a.b[0].slice0 = 0u;
         a.nslices = (a.b[0].n + 63u) / 64u;
-        constexpr int ABL = ((SRVX & 16) ? kAblNoProbe : 0) | ((SRVX & 32) ? kAblNoStore : 0) |
-                            ((SRVX & 64) ? kAblHotBuckets : 0) | ((SRVX & 128) ? kAblNoSearch : 0) |
-                            ((SRVX & 256) ? kAblStamps : 0);
-        if constexpr ((SRVX & 256) != 0) {
-            a.sel = reinterpret_cast<const uint32_t *>(sa.counters + 16u + 32u * 8u + (q & 31u) * 16u);
-            abl_stamp<ABL>(a, (int)(threadIdx.x & 63u), 11);  // the request's words read, RxArgs built
-        }
-        if constexpr (!(SRVX & 1)) rx_body<MODE, kDescList, false, false, true, ABL>(a, blockIdx.x, P);
-        if constexpr ((SRVX & 8) != 0) stamp[2] = (unsigned long long)wall_clock64();
-        if constexpr ((SRVX & 512) != 0) {  // the body again, its code and data now cached
-            rx_body<MODE, kDescList, false, false, true, ABL>(a, blockIdx.x, P);
-            stamp[7] = (unsigned long long)wall_clock64();
-        }
+        rx_body<MODE, kDescList, false, false, true>(a, blockIdx.x, P);
         // Every wave's stores have reached the L2 (vmcnt), then ONE system-scope release per
         // workgroup writes this XCD's L2 back (buffer_wbl2 covers the whole cache, so one
         // per workgroup covers its four waves; it used to run once per wave and once more
@@ -2030,17 +2061,8 @@ __global__ __launch_bounds__(256, 3) void rx_server(SrvArgs sa)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            if constexpr ((SRVX & 8) != 0) stamp[3] = (unsigned long long)wall_clock64();
-            if constexpr (!(SRVX & 4)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr ((SRVX & 8) != 0) {
-                stamp[4] = (unsigned long long)wall_clock64();
-                stamp[6] = __builtin_amdgcn_s_memtime();
-                if (blockIdx.x == 0) {
-                    unsigned long long *d = sa.counters + 16u + (q & 31u) * 8u;  // vector stores
-                    for (int k = 0; k < 8; ++k) d[k] = stamp[k];
-                }
-            }
             bool lastp = true;
             if (P > 1u) {
                 lastp = atomicAdd(&sa.ctl->fin, 1u) + 1u == P;
@@ -2073,6 +2095,8 @@ inline hipError_t rx_args(const LaunchRx &L, RxArgs &a, RxGrid &g)
     a.t = L.table;
     a.counters = L.counters;
     a.stride64 = L.stride64;
+    a.pay_arena = L.pay_arena;
+    a.pay_msgs = L.pay_msgs;
     if (L.nbursts > kMaxBursts) return hipErrorInvalidValue;
     uint32_t nslices = 0;
     for (uint32_t k = 0; k < L.nbursts; ++k) {
@@ -2092,7 +2116,7 @@ inline hipError_t rx_args(const LaunchRx &L, RxArgs &a, RxGrid &g)
     if (g.blocks > L.max_blocks) g.blocks = L.max_blocks;
     // long launches (C2 as 16 bursts: 85 slices per wave) prefetch all-small runs two slices
     // deep; short ones (one 2^20-frame burst: 5.3 per wave) measured slower with it (§5)
-    g.deep = nslices >= kDeepSlicesPerWave * g.blocks * 4u;
+    g.deep = nslices >= kDeepSlicesPerWave * g.blocks * 4u && !L.pay_msgs;  // (PAY kernels: one depth)
     return hipSuccess;
 }
 

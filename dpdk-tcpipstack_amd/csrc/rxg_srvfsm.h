@@ -7,9 +7,14 @@
 //   bool exited()                the kernel has left its loop (stop or idle)
 //   void write(q)                post request number q (mailbox words; the request body is
 //                                the port's business)
+//   void cancel(q)               no kernel is resident: make request q (still in the mailbox)
+//                                one the next kernel will not serve (its `done` reads q)
 //   void request_stop()          ask the kernel to leave its loop
 //   int  launch()                start a kernel (the previous one has exited or none ran;
-//                                its stream is synchronised first): 0 or a negative errno
+//                                its stream is synchronised first): 0 or a negative errno.
+//                                It resets exited() to false BEFORE the kernel starts: the
+//                                machine synchronises a stream on the strength of exited()
+//                                alone (tests/srvfsm_check.cpp holds it to that)
 //   void sync()                  wait for the exited kernel's stream (returns at once: the
 //                                kernel has left its loop)
 //
@@ -56,11 +61,16 @@ struct SrvFsm {
         return 0;
     }
 
-    // A kernel ready to serve: -EIO while a failed kernel is still resident.
+    // A kernel ready to serve: -EIO while a failed kernel is still resident.  Relaunching
+    // after a failure first cancels the request that timed out: its caller was told it
+    // failed (and may have freed its output), so no later kernel may serve it.
     int ready(Port &p)
     {
         if (phase == SrvPhase::Failed) {
             if (!wait_exited(p, exit_timeout)) return -EIO;
+            p.sync();
+            phase = SrvPhase::Down;
+            p.cancel(seq);
             return relaunch(p);
         }
         if (phase == SrvPhase::Down || p.exited()) return relaunch(p);

@@ -19,7 +19,35 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PRODUCT_LIB = os.path.join(_HERE, "librxg.so")
+# RXG_LIB swaps in another build (an experiment or an older library for an A/B) only with
+# the explicit opt-in RXG_LIB_OVERRIDE=1: a stray RXG_LIB must not put another library under
+# the tests, smoke() or bench.py.  load_library() refuses it otherwise.
 LIB_PATH = os.environ.get("RXG_LIB") or _PRODUCT_LIB
+
+
+def source_hash(root: str = os.path.dirname(_HERE)) -> str:
+    """The product sources' hash exactly as the Makefile compiles it into rxg_build_info
+    (src=...): sha256 over csrc/*.h, *.hip, *.cpp in sorted order, then include/rxg.h."""
+    import glob
+    import hashlib
+    csrc = os.path.join(root, "csrc")
+    files = sorted(os.path.relpath(p, root) for ext in ("h", "hip", "cpp")
+                   for p in glob.glob(os.path.join(csrc, "*." + ext)))
+    h = hashlib.sha256()
+    for rel in files + [os.path.join("..", "include", "rxg.h")]:
+        with open(os.path.join(root, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_provenance(lib=None) -> dict:
+    """What the loaded library says it was built from, and whether that is this tree."""
+    lib = lib or load_library()
+    info = lib.rxg_build_info().decode()
+    src = next((w[4:] for w in info.split() if w.startswith("src=")), None)
+    tree = source_hash()
+    return {"build": info, "lib": os.path.abspath(_loaded_path or LIB_PATH), "source_hash": tree,
+            "build_matches_tree": src == tree}
 
 # ---------------------------------------------------------------- constants (rxg.h) ---
 ETHER_TYPE_IPV4 = 0x0800
@@ -167,6 +195,11 @@ class PayloadOut(C.Structure):
                 ("arena_used", C.c_void_p)]
 
 
+class PayloadSlots(C.Structure):
+    """rxg_payload_slots: the fused burst's payload arena (the pool's geometry) and messages."""
+    _fields_ = [("arena", C.c_void_p), ("msgs", C.c_void_p)]
+
+
 class SynthParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("n", C.c_uint32), ("nflows", C.c_uint32),
                 ("dst_ip_host", C.c_uint32), ("dport", C.c_uint16), ("mix", C.c_uint16),
@@ -200,14 +233,18 @@ CFG_STREAMS_OUTLIVE_WRITES = 0x2  # caller streams stay valid until the next tab
 
 # ------------------------------------------------------------------------- loading ---
 _lib = None
+_loaded_path = None
 
 
 def load_library(path: str = LIB_PATH):
     """Load librxg.so.  torch (if installed) is imported first so that librxg binds to the
     same HIP runtime copy torch loaded (one HIP runtime per process)."""
-    global _lib
+    global _lib, _loaded_path
     if _lib is not None:
         return _lib
+    if os.path.abspath(path) != _PRODUCT_LIB and os.environ.get("RXG_LIB_OVERRIDE") != "1":
+        raise RxgError(f"refusing to load {path} in place of the product library {_PRODUCT_LIB}: "
+                       "set RXG_LIB_OVERRIDE=1 as well to load another build")
     if not os.path.exists(path):
         raise RxgError(f"librxg.so not built: {path} (run __graft_entry__.build())")
     if "torch" not in sys.modules:
@@ -261,6 +298,7 @@ def load_library(path: str = LIB_PATH):
         "rxg_ether_in": (C.c_int, [vp, C.POINTER(HandoffOps), vp, vp, C.c_uint16]),
         "rxg_replay_stats": (C.c_int, [vp, vp]),
         "rxg_payload_gather_dev": (C.c_int, [vp, C.POINTER(PayloadOut), vp]),
+        "rxg_rx_burst_payload_dev": (C.c_int, [vp, C.POINTER(DevBatch), C.POINTER(PayloadSlots), vp]),
         "rxg_rcv_set": (C.c_int, [vp, i32, u32, u32]),
         "rxg_payload_take": (C.c_int, [vp, i32, u32, u32, C.POINTER(PayloadMsg)]),
         "rxg_synth_dev": (C.c_int, [vp, C.POINTER(SynthParams), vp, u64, vp, vp, vp,
@@ -315,6 +353,7 @@ def load_library(path: str = LIB_PATH):
     if lib.rxg_abi_version() != ABI_VERSION:
         raise RxgError(f"librxg ABI version {lib.rxg_abi_version()}, binding expects {ABI_VERSION}")
     _lib = lib
+    _loaded_path = path
     return lib
 
 
@@ -587,6 +626,14 @@ class Engine:
         b = DevBatch(frames, off64, lens, n, rec_kind, out)
         _check(_lib.rxg_rx_burst_dev(self.ctx, C.byref(b), stream), "rxg_rx_burst_dev")
 
+    def rx_burst_payload_dev(self, frames: int, off64: int, lens: int, n: int, out: int, arena: int,
+                             msgs: int, rec_kind: int = REC16, stream=None):
+        """rxg_rx_burst_payload_dev: the burst and its payload hand-off in one pass; payload
+        lines to `arena` (the frame pool's geometry), one rxg_payload_msg per frame to msgs."""
+        b = DevBatch(frames, off64, lens, n, rec_kind, out)
+        p = PayloadSlots(arena, msgs)
+        _check(_lib.rxg_rx_burst_payload_dev(self.ctx, C.byref(b), C.byref(p), stream), "rxg_rx_burst_payload_dev")
+
     def rx_bursts_dev(self, frames: int, bursts, rec_kind: int = REC16, stream=None):
         """bursts: [(off64 ptr, len ptr, n, out ptr), ...] of one frame pool, one launch."""
         arr = (DevBurst * max(len(bursts), 1))(*[DevBurst(o, l, n, 0, out) for o, l, n, out in bursts])
@@ -687,6 +734,28 @@ class Engine:
         used = int(du.download(np.uint64, 1)[0])
         arena = da.download(np.uint8, min(arena_cap, used)) if arena_cap else np.zeros(0, np.uint8)
         return arena, msgs, used
+
+    def rx_burst_payload(self, frames, rec_kind: int = REC16, arena_fill: int | None = None):
+        """Host frames through rxg_rx_burst_payload_dev (packed, uploaded): returns (records of
+        rec_kind,
+        payload arena as np.uint8 -- the pool's geometry -- , msgs, (arena, off64, lens) as
+        packed).  arena_fill: the payload arena's bytes before the call (None: zeros).  The
+        device buffers live until the next call (the replay reads the batch, rxg_payload_take
+        the messages)."""
+        for d in getattr(self, "_pf_bufs", ()):
+            d.free()
+        arena, off, lens = pack_arena(frames)
+        n = len(frames)
+        da, do, dl = self.to_device(arena), self.to_device(off), self.to_device(lens)
+        dr, dm = self.alloc(max(n, 1) * rec_kind), self.alloc(max(n, 1) * 16)
+        dp = self.alloc(max(arena.nbytes, 64))
+        dp.upload(np.full(max(arena.nbytes, 64), 0 if arena_fill is None else arena_fill, dtype=np.uint8))
+        self._pf_bufs = (da, do, dl, dr, dm, dp)
+        self.rx_burst_payload_dev(da.ptr, do.ptr, dl.ptr, n, dr.ptr, dp.ptr, dm.ptr, rec_kind)
+        self.sync()
+        recs = dr.download(rec_dtype(rec_kind), n)  # as the kernel wrote them (rec8_expand for REC8)
+        msgs = dm.download(PAYLOAD_MSG_DTYPE, n) if n else np.zeros(0, PAYLOAD_MSG_DTYPE)
+        return recs, dp.download(np.uint8, arena.nbytes), msgs, (arena, off, lens)
 
     def rcv_set(self, idx: int, cur_seq: int, pairs_pending: bool):
         _check(_lib.rxg_rcv_set(self.ctx, idx, cur_seq & 0xFFFFFFFF, int(bool(pairs_pending))),

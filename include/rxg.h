@@ -221,8 +221,13 @@ typedef struct rxg_config {
 #define RXG_CFG_STREAMS_OUTLIVE_WRITES 0x2u
 
 int rxg_abi_version(void);
+/* "rxg src=<16 hex: sha256 of the product sources> rev=<git revision>[+dirty] built=<date>
+   gfx950": which sources the library was built from (rxg.source_hash() recomputes src=). */
 const char *rxg_build_info(void);
 int rxg_init(const rxg_config *cfg, rxg_ctx **out);
+/* 0, or -EIO when a latency-mode server kernel that missed its time limit is still resident
+   after bounded retries of rxg_server_stop: the context and every buffer that kernel can
+   reach are then left allocated (leaked), never freed under it; the handle is dead either way. */
 int rxg_fini(rxg_ctx *ctx);
 /* Block until all work queued on the context's stream is done. */
 int rxg_sync(rxg_ctx *ctx);
@@ -565,7 +570,8 @@ enum rxg_payload_flag {
 };
 
 typedef struct rxg_payload_msg {
-    uint64_t arena_off;  /* payload at arena + arena_off, 16-byte aligned                    */
+    uint64_t arena_off;  /* payload at arena + arena_off: 16-byte aligned (gather), or the
+                            payload's offset in the frame pool (rxg_rx_burst_payload_dev)   */
     uint32_t len;        /* Length = datalen (tcp_states.c:111), bytes at frame + 34 +
                             (data_off >> 4) * 4 (tcp_windows.c:164-166); 0 if not gathered   */
     uint32_t flags;      /* RXG_PM_*                                                        */
@@ -591,6 +597,23 @@ typedef struct rxg_payload_out {
    One gather is in flight per context: a gather waits (on the device) for the previous
    one, whatever streams they were issued on. */
 int rxg_payload_gather_dev(rxg_ctx *ctx, const rxg_payload_out *o, void *stream);
+
+/* The burst and its payload hand-off in ONE pass over the frames (rxg_rx_burst_dev followed
+   by rxg_payload_gather_dev reads every payload byte twice).  The same records and counters
+   as rxg_rx_burst_dev, and one message per frame for exactly the frames the gather takes
+   (same len and flags; the message bytes are the same payload bytes), but each payload stays
+   where its frame puts it: the arena has the frame pool's geometry.  For a candidate frame i
+   the 64-byte lines of [frames + 64*off64[i] + start, + datalen) are written, unchanged, at
+   the same offsets from `arena` (start = 34 + data_off*4), and msgs[i].arena_off = 64*off64[i]
+   + start (not 16-byte aligned); other frames' lines are not written.  `arena` must hold
+   64*(max off64[i]) + len rounded up to 64 bytes, and be 64-byte aligned; msgs 16-byte
+   aligned.  rxg_payload_take then answers from these messages, as after a gather.
+   Asynchronous on `stream`. */
+typedef struct rxg_payload_slots {
+    void *arena;            /* dev: the pool's geometry (see above)               */
+    rxg_payload_msg *msgs;  /* dev, b->n messages                                   */
+} rxg_payload_slots;
+int rxg_rx_burst_payload_dev(rxg_ctx *ctx, const rxg_dev_batch *b, const rxg_payload_slots *p, void *stream);
 
 /* Receive-window mirror: ReceiveWindow.CurrentSequenceNumber of tcbs[idx] and whether its
    SeqPairs list is non-empty (tcp_windows.h:37-44).  The stack calls it wherever it

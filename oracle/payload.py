@@ -12,7 +12,8 @@ whether PushData is reached and takes the segment is decided at replay time).  F
 whose payload would run past the frame (the reference copies stale mbuf bytes there),
 records marked RXG_F_TRUNC and datalen <= 0 are left to the stack.  Layout (rxg's):
 packet order, each message 16-byte aligned and zero padded; frames past the arena
-capacity are not gathered.
+capacity are not gathered.  slots(): the same messages as rxg_rx_burst_payload_dev lays them
+out (the fused burst + hand-off: each payload stays at its frame's offset in the pool).
 """
 from __future__ import annotations
 
@@ -50,3 +51,20 @@ def gather(frames, recs, arena_cap: int):
             parts.append(p + b"\0" * (r16 - len(p)))
         off += r16
     return msgs, np.frombuffer(b"".join(parts), dtype=np.uint8), off
+
+
+def slots(frames, recs, off64):
+    """Expected messages of rxg_rx_burst_payload_dev: the candidates of gather(), each at its
+    offset in the frame pool (arena_off = 64 * off64[i] + 34 + data_off * 4), same len and
+    flags; returns (msgs, [payload bytes or None per frame])."""
+    n = len(frames)
+    msgs = np.zeros(n, dtype=MSG_DTYPE)
+    pays = []
+    for i, f in enumerate(frames):
+        p = candidate(f, recs[i])
+        pays.append(p)
+        if p is None:
+            continue
+        start = 34 + (f[46] >> 4) * 4
+        msgs[i] = (int(off64[i]) * 64 + start, len(p), PM_GATHERED | (PM_REF_OVERSIZE if len(p) >= 1000 else 0))
+    return msgs, pays

@@ -7,7 +7,7 @@ sync; host wall time per sync, per write.  Run once with the product library (O(
 patches) and once with the experiment library under RXG_MIRROR_REBUILD=1 (round 1: every
 sync rebuilds and uploads the whole table):
   python scripts/mirrorbench.py            # product
-  RXG_LIB=dpdk-tcpipstack_amd/rxg/librxg_exp.so RXG_MIRROR_REBUILD=1 python scripts/mirrorbench.py
+  RXG_LIB_OVERRIDE=1 RXG_LIB=dpdk-tcpipstack_amd/rxg/librxg_exp.so RXG_MIRROR_REBUILD=1 python scripts/mirrorbench.py
 Prints one JSON line per (Ntcb, k)."""
 import json
 import os

@@ -13,6 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dpdk-tcpipstack_amd")]
 # the experiment library (make -C dpdk-tcpipstack_amd experiments): the variant switches
 os.environ.setdefault("RXG_LIB", os.path.join(ROOT, "dpdk-tcpipstack_amd", "rxg", "librxg_exp.so"))
+os.environ.setdefault("RXG_LIB_OVERRIDE", "1")  # the experiment library, on purpose (rxg.load_library)
 import rxg  # noqa: E402
 
 WL = {"c3": (1500, 1000, 0), "c2": (64, 1, 0), "c4": (0, 65536, 1)}

@@ -7,23 +7,50 @@
 #include <cerrno>
 #include <chrono>
 #include <cstdio>
+#include <vector>
 
 #include "rxg_srvfsm.h"
 
+// A scripted device with a mailbox that persists across launches, like the real one: the
+// last request written stays there, and a kernel starts from `done` (rx_server: last =
+// ret->done) and serves any request numbered above it.
 struct FakePort {
     unsigned long long done_ = 0;
+    unsigned long long mbox_seq = 0;  // the request number in the mailbox
+    unsigned long long last = 0;      // the resident kernel's last request seen
     bool exited_ = true;     // no kernel yet
     bool serving = true;     // a running kernel answers each request at once
     bool obeys_stop = true;  // a stop request makes it exit
-    int launches = 0, syncs = 0, stops = 0, writes = 0;
+    int launches = 0, syncs = 0, stops = 0, writes = 0, cancels = 0;
     bool synced_while_resident = false;
+    bool exit_seen = true;   // exited() has read true since the last launch (none yet: true)
+    std::vector<unsigned long long> served;  // every request a kernel served, in order
 
     unsigned long long done() const { return done_; }
-    bool exited() const { return exited_; }
+    bool exited() const
+    {
+        if (exited_) const_cast<FakePort *>(this)->exit_seen = true;
+        return exited_;
+    }
+    void serve()
+    {
+        if (!exited_ && serving && mbox_seq > last) {
+            last = mbox_seq;
+            done_ = mbox_seq;
+            served.push_back(mbox_seq);
+        }
+    }
     void write(unsigned long long q)
     {
         ++writes;
-        if (!exited_ && serving) done_ = q;
+        mbox_seq = q;
+        serve();
+    }
+    void cancel(unsigned long long q)
+    {
+        assert(exited_);  // only with no kernel resident
+        ++cancels;
+        done_ = q;
     }
     void request_stop()
     {
@@ -32,14 +59,26 @@ struct FakePort {
     }
     int launch()
     {
+        // the Port contract: a kernel is launched only after the previous one was seen to
+        // exit (or none ran), and launch() resets exited before the kernel runs
+        assert(exit_seen);
         ++launches;
         exited_ = false;
+        exit_seen = false;
+        last = done_;
+        serve();  // the new kernel polls the mailbox at once
         return 0;
     }
     void sync()
     {
         ++syncs;
         if (!exited_) synced_while_resident = true;  // would block forever on a real stream
+    }
+    bool was_served(unsigned long long q) const
+    {
+        for (auto s : served)
+            if (s == q) return true;
+        return false;
     }
 };
 
@@ -95,8 +134,14 @@ int main()
         p.exited_ = true;
         p.serving = true;
         p.obeys_stop = true;
+        const unsigned long long timed_out = f.seq - 0;  // the request that failed, still in the mailbox
+        assert(p.mbox_seq == timed_out && !p.was_served(timed_out));
         assert(f.post(p) == 0 && f.phase == rxg::SrvPhase::Up && p.launches == launches + 1);
-        assert(p.done_ == f.seq);
+        assert(p.done_ == f.seq && p.cancels == 1);
+        // the relaunched kernel served the new request only, never the
+        // one whose caller was told -ETIMEDOUT
+        assert(!p.was_served(timed_out));
+        assert(p.served.back() == f.seq);
         assert(f.stop(p) == 0 && f.phase == rxg::SrvPhase::Down);
         assert(!p.synced_while_resident);
     }
@@ -107,9 +152,33 @@ int main()
         assert(f.post(p) == 0);
         p.serving = false;
         assert(f.post(p) == -ETIMEDOUT && p.exited_);
+        const unsigned long long timed_out = f.seq;
         p.serving = true;
         assert(f.post(p) == 0 && p.launches == 2);
+        assert(!p.was_served(timed_out) && p.served.back() == f.seq);
         assert(!p.synced_while_resident);
+    }
+    {  // the mailbox persists: after a timeout, two more posts, each served exactly once
+        FakePort p;
+        Fsm f;
+        f.serve_timeout = ms(10);
+        assert(f.post(p) == 0 && f.post(p) == 0);
+        p.serving = false;
+        assert(f.post(p) == -ETIMEDOUT);
+        const unsigned long long timed_out = f.seq;
+        p.serving = true;
+        assert(f.post(p) == 0 && f.post(p) == 0);
+        const std::vector<unsigned long long> want = {1, 2, timed_out + 1, timed_out + 2};
+        assert(p.served == want);
+        assert(!p.synced_while_resident);
+    }
+    {  // an idle exit is not a failure: the request posted to the exited kernel is served by
+       // the relaunched one (no cancel)
+        FakePort p;
+        Fsm f;
+        assert(f.post(p) == 0);
+        p.exited_ = true;  // idle exit, unobserved until the next post
+        assert(f.post(p) == 0 && p.cancels == 0 && p.served.back() == f.seq);
     }
     {  // stop with nothing launched
         FakePort p;

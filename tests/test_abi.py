@@ -50,6 +50,42 @@ def test_abi_version_and_build_info():
     assert b"gfx950" in lib.rxg_build_info()
 
 
+def test_build_info_names_this_source_tree():
+    """rxg_build_info carries the product sources' hash (Makefile SRC_HASH); the library under
+    test was built from exactly the sources in this tree, and the hash is computed the same
+    way on both sides."""
+    prov = rxg.build_provenance()
+    assert "src=" + prov["source_hash"] in prov["build"], prov
+    assert prov["build_matches_tree"], prov
+    assert " rev=" in prov["build"]
+    assert prov["lib"] == os.path.abspath(rxg._PRODUCT_LIB)
+
+
+def _load_in_child(env_extra):
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import rxg\n"
+            "try:\n    rxg.load_library(); print('LOADED', rxg._loaded_path)\n"
+            "except rxg.RxgError as e:\n    print('REFUSED', e)\n") % os.path.join(ROOT, "dpdk-tcpipstack_amd")
+    env = {k: v for k, v in os.environ.items() if k not in ("RXG_LIB", "RXG_LIB_OVERRIDE")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                          timeout=120).stdout
+
+
+def test_rxg_lib_override_needs_opt_in():
+    """RXG_LIB alone never swaps the product library: it is refused
+    loudly; with RXG_LIB_OVERRIDE=1 the named build is loaded; unset, the product one."""
+    other = os.path.join(ROOT, "dpdk-tcpipstack_amd", "rxg", "librxg_exp.so")
+    if not os.path.exists(other):
+        pytest.skip("experiment library not built")
+    out = _load_in_child({"RXG_LIB": other})
+    assert out.startswith("REFUSED") and "RXG_LIB_OVERRIDE=1" in out, out
+    out = _load_in_child({"RXG_LIB": other, "RXG_LIB_OVERRIDE": "1"})
+    assert out.strip() == "LOADED " + other, out
+    out = _load_in_child({})
+    assert out.strip() == "LOADED " + rxg._PRODUCT_LIB, out
+
+
 def test_struct_layouts_match_header():
     hdr = open(HEADER).read()
     src = r'''
@@ -177,33 +213,37 @@ EXPERIMENT_SWITCHES = [b"RXG_VARIANT", b"RXG_NOCOUNT", b"RXG_PG_VARIANT", b"RXG_
 
 
 def _kernel_instantiations(path):
-    """(MODE, DESC, MULTI, DEEP, ABL) of every rx_kernel in the library's gfx950 code object
-    (csrc/rxg_rx.h: rx_kernel<MODE, DESC, MULTI, DEEP, ABL>)."""
+    """(MODE, DESC, MULTI, DEEP, PAY) of every rx_kernel in the library's gfx950 code object
+    (csrc/rxg_rx.h: rx_kernel<MODE, DESC, MULTI, DEEP, PAY>)."""
     data = open(path, "rb").read()
     return {tuple(int(x) for x in m) for m in
-            re.findall(rb"rx_kernelILi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELi(\d+)EEEv", data)}
+            re.findall(rb"rx_kernelILi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELb(\d)EEEv", data)}
 
 
 # The product kernels: round 3's set (every record kind single / multi-burst, the two-deep
-# REC8 / REC16 forms, tx, the REC16 re-classification through a selection list) plus the
-# fixed-stride forms (DESC 2, rxg_rx_bursts_strided_dev).
+# REC8 / REC16 forms, tx, the REC16 re-classification through a selection list), the
+# fixed-stride forms (DESC 2, rxg_rx_bursts_strided_dev), and round 5's fused payload
+# hand-off (PAY 1, rxg_rx_burst_payload_dev: one burst, every record kind, list or stride).
 PRODUCT_KERNELS = ({(m, d, mu, dp, 0) for m in (8, 16) for d in (0, 2) for mu in (0, 1) for dp in (0, 1)}
                    | {(48, d, mu, 0, 0) for d in (0, 2) for mu in (0, 1)}
-                   | {(0, 0, 0, 0, 0), (16, 1, 0, 0, 0)})
+                   | {(0, 0, 0, 0, 0), (16, 1, 0, 0, 0)}
+                   | {(m, d, 0, 0, 1) for m in (8, 16, 48) for d in (0, 2)})
 
 
 def test_product_library_has_no_experiment_switches():
     """librxg.so reads no environment variable that changes what a burst computes and holds
-    only the production kernels: no ablation (ABL 0 everywhere), exactly PRODUCT_KERNELS.
-    The ablation kernels live in the experiment build (librxg_exp.so, make experiments,
-    csrc/rxg_kernels_exp.hip) that scripts/kbench.py loads."""
+    only the production kernels, exactly PRODUCT_KERNELS (no ablation
+    template parameter is left in rx_kernel / rx_server; their round-2..4 measurements are in
+    DESIGN.md §9).  Experiment variants live in the experiment build (librxg_exp.so, make
+    experiments, csrc/rxg_kernels_exp.hip) that scripts/kbench.py loads."""
     data = open(rxg.LIB_PATH, "rb").read()
     for sw in EXPERIMENT_SWITCHES:
         assert sw not in data, sw
     inst = _kernel_instantiations(rxg.LIB_PATH)
     assert inst == PRODUCT_KERNELS, sorted(inst ^ PRODUCT_KERNELS)
-    servers = set(re.findall(rb"rx_serverILi(\d+)ELi(\d+)EEEv", data))
-    assert servers == {(b"8", b"0"), (b"16", b"0"), (b"48", b"0")}, servers
+    servers = set(re.findall(rb"rx_serverILi(\d+)EEEv", data))
+    assert servers == {b"8", b"16", b"48"}, servers
+    assert not re.findall(rb"rx_serverILi\d+ELi", data)  # no second (stamp / ablation) parameter
     assert re.findall(rb"pg_gather", data)
 
 
@@ -214,16 +254,18 @@ def test_experiment_library_is_separate():
     data = open(exp, "rb").read()
     assert all(sw in data for sw in EXPERIMENT_SWITCHES)
     inst = _kernel_instantiations(exp)
-    assert PRODUCT_KERNELS <= inst and any(abl != 0 for *_, abl in inst)
+    assert PRODUCT_KERNELS <= inst
 
 
 def test_kernel_source_has_no_experiment_branches():
-    """the product kernel source keeps no experiment scaffolding: no
-    RXG_EXPERIMENTS blocks, no STRIP bits, and rx_body takes at most 6 template parameters."""
+    """the product kernel source keeps no experiment
+    scaffolding: no RXG_EXPERIMENTS blocks, no STRIP / ablation / stamp bits, and rx_body
+    takes at most 6 template parameters."""
     csrc = os.path.join(ROOT, "dpdk-tcpipstack_amd", "csrc")
     for f in ("rxg_kernels.hip", "rxg_rx.h"):
         src = open(os.path.join(csrc, f)).read()
-        assert "RXG_EXPERIMENTS" not in src and "STRIP" not in src, f
+        for word in ("RXG_EXPERIMENTS", "STRIP", "ABL", "SRVX", "kAbl", "abl_stamp"):
+            assert word not in src, (f, word)
     body = open(os.path.join(csrc, "rxg_rx.h")).read()
     m = re.search(r"template <([^>]*)>\s*__device__ __forceinline__ void rx_body\(", body)
     assert m and len(m.group(1).split(",")) <= 6, m and m.group(1)

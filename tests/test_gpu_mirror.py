@@ -257,3 +257,47 @@ def test_caller_stream_destroyed_before_the_next_write(lazy):
             if isinstance(v, rxg.DevArray):
                 v.free()
         engine.close()
+
+
+def test_rejected_launch_keeps_the_previous_burst_replayable():
+    """under RXG_CFG_STREAMS_OUTLIVE_WRITES a launch on an unregistered stream
+    is refused before anything changes (no mirror sync, replay state kept), so rxg_rx_replay
+    of the burst before it still runs, and calls the hand-off for every dispatched packet."""
+    import ctypes as C
+    import pktgen
+    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln)
+    hip = C.CDLL(path)
+    engine = rxg.Engine(device=0, max_batch=4096, max_bytes=8 << 20, flags=rxg.CFG_STREAMS_OUTLIVE_WRITES)
+    rows, frames = pktgen.parity_set(11, 600)
+    dev = engine.synth(n=256, nflows=4, len_a=64, seed=80)
+    out = engine.alloc(256 * 16)
+    st = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(st)) == 0
+    try:
+        tcb, live = pktgen.table_arrays(rows)
+        engine.tcb_load(tcb, live)
+        engine.arp_disable()
+        recs = engine.rx_burst(frames, rxg.REC16)
+        with pytest.raises(rxg.RxgError, match="not registered"):
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, 256, out.ptr, 16, st.value)
+        seen = []
+
+        def tcpswitch(u, idx, state, tcp, ip, m):
+            seen.append(idx)
+            return 0
+        ops = rxg.HandoffOps(None, rxg.HANDOFF_FREE(), rxg.HANDOFF_ARP_IN(), rxg.HANDOFF_GET_MAC(),
+                             rxg.HANDOFF_ADD_MAC(), rxg.HANDOFF_SEND_RESET(), rxg.HANDOFF_ON_SEGMENT(),
+                             rxg.HANDOFF_TCPSWITCH(tcpswitch))
+        bufs = [C.create_string_buffer(f, max(len(f), 64)) for f in frames]
+        ptrs = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
+        lib = rxg.load_library()
+        assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, len(bufs), 16) == 0
+        disp = recs["tcb_idx"][recs["verdict"] == rxg.V_DISPATCH]
+        assert seen == disp.tolist() and len(seen) > 100
+    finally:
+        assert hip.hipStreamDestroy(st) == 0
+        out.free()
+        for v in dev.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()
+        engine.close()
