@@ -900,6 +900,8 @@ def main():
         # the other record kind on the same ring
         legs[f"c2_64B_1flow_multiburst_rec{other}"] = multiburst_leg(eng, max(5, args.steps // 5), 2, device,
                                                                      seed, rec=other)
+        eng.tcb_load(tcb, live)  # the headline's table again (the legs above loaded theirs)
+        eng.tcb_sync()
         legs["payload_gather"] = payload_leg(eng, wl, args.steps, 2)
         legs["c3_rx_payload_fused"] = fused_leg(eng, wl, args.steps, 2)
         two = legs["payload_gather"]["kernels_us"] + (region_ms / args.steps * 1e3)

@@ -4,7 +4,9 @@
 //
 // The round-2..4 ablation kernels (no probe / no stores / no classify / stamped server
 // phases) were removed in round 5 with their template parameters; what they measured is in
-// DESIGN.md §9.R3 / §9.R4 and profiles/r03, r04.
+// DESIGN.md §9.R3 / §9.R4 and profiles/r03, r04.  So were round 5's fused payload forms
+// (RXG_VARIANT 101-107: plain / chunk-granular / pipelined / 4-waves stores; DESIGN.md §5.F,
+// profiles/r05/fused/).
 #include <hip/hip_runtime.h>
 
 #include "rxg_kernels.h"
