@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""A/B of the fused rx + payload hand-off forms (rxg_rx_burst_payload_dev) in one process,
-through the experiment library: RXG_VARIANT 0 = production (PAY form 1), 101 / 102 / 103 =
-forms 2 / 3 / 4 (csrc/rxg_kernels_exp.hip).  Per workload (C3 1500 B / 1 K flows, C4 IMIX /
-64 K flows, C2 64 B / 1 flow; 2^20 frames, rotating batches as bench.py), the mean kernel time
-over K launches (one event pair around them), interleaved rounds, and a check that every form
-writes the production form's records and messages.  One JSON line per (round, workload, form).
-  python scripts/fusedbench.py [--variants 0,101,102,103] [--rounds 3] [--steps 20]"""
+"""A/B of the fused rx + payload hand-off (rxg_rx_burst_payload_dev) in one process, through
+the experiment library: RXG_VARIANT 0 = production; round 5's forms 101-107 (plain /
+chunk-granular / pipelined / 4-waves stores) were measured with it and removed again
+(profiles/r05/fused/).  A variant "V@G" caps the grid at G workgroups.  Per workload (C3
+1500 B / 1 K flows, C4 IMIX / 64 K flows, C2 64 B / 1 flow; 2^20 frames, rotating batches as
+bench.py), the mean kernel time over K launches (one event pair around them), interleaved
+rounds, and a check that every variant writes the first one's records and messages; --shifts
+places the payload arena at other offsets from the pool.  One JSON line per measurement.
+  python scripts/fusedbench.py [--variants 0,0@512] [--rounds 3] [--steps 20] [--copy-ref]"""
 import argparse
 import json
 import os
@@ -25,7 +27,7 @@ WL = {"c3": (1500, 1000, 0, 2), "c4": (0, 65536, 1, 3), "c2": (64, 1, 0, 16)}
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,101,102,103", help="forms (RXG_VARIANT), each optionally @grid")
+    ap.add_argument("--variants", default="0", help="forms (RXG_VARIANT), each optionally @grid")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--workloads", default="c3,c4,c2")
