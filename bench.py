@@ -423,22 +423,25 @@ def payload_leg(eng, wl, steps, warmup):
             d.free()
 
 
-def fused_leg(eng, wl, steps, warmup):
+def fused_leg(eng, wl, steps, warmup, by_reference=False):
     """The burst and its payload hand-off in ONE pass (rxg_rx_burst_payload_dev, DESIGN.md
     §5.F) over the workload's rotating batches, against the two-pass form (rxg_rx_burst_dev,
     then rxg_payload_gather_dev reading every payload byte again).  One event pair around the
     launches.  Algorithmic bytes per launch = the frame bytes read + the payload bytes handed
     off + a 16-byte message and a record per frame (the two-pass form moves the same plus
     the payload read a second time)."""
-    arenas = [eng.alloc(b["arena_bytes"]) for b in wl.batches]
+    # by_reference: no arena -- each message names its payload in the pool itself (nothing
+    # copied; rxg.h rxg_rx_burst_payload_dev), the algorithmic bytes without the payload write
+    arenas = [None if by_reference else eng.alloc(b["arena_bytes"]) for b in wl.batches]
     msgs = eng.alloc(wl.n * 16)
     pl = (wl.lens.astype(np.int64) - 54).clip(min=0)  # synthetic frames: IHL 5, data_off 5
     dl = int(pl.sum())
     try:
         def launch(i):
             b = wl.batches[i % wl.copies]
+            ar = arenas[i % wl.copies]
             eng.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, wl.n, wl.out.ptr,
-                                     arenas[i % wl.copies].ptr, msgs.ptr, wl.rec)
+                                     ar.ptr if ar else None, msgs.ptr, wl.rec)
         for i in range(warmup):
             launch(i)
         eng.sync()
@@ -454,8 +457,9 @@ def fused_leg(eng, wl, steps, warmup):
         eng.event_destroy(e1)
         c = eng.counters()
         m = msgs.download(rxg.PAYLOAD_MSG_DTYPE, wl.n)
-        alg = wl.bytes_per_batch + dl + (16 + wl.rec) * wl.n
-        tb = traffic_of("c3_rx_payload_fused", wl.n, wl.rec)[0] if wl.name == "c3_1500B_1Kflows" else None
+        alg = wl.bytes_per_batch + (0 if by_reference else dl) + (16 + wl.rec) * wl.n
+        tb = (traffic_of("c3_rx_payload_fused", wl.n, wl.rec)[0]
+              if wl.name == "c3_1500B_1Kflows" and not by_reference else None)
         return {"kernel_us": round(k * 1e6, 2), "mpps": round(wl.n / k / 1e6, 1),
                 "payload_bytes": dl, "algorithmic_bytes_per_launch": alg,
                 "traffic_bytes_per_launch": tb,
@@ -464,7 +468,8 @@ def fused_leg(eng, wl, steps, warmup):
                            and (m["len"] == pl).all())}
     finally:
         for d in arenas + [msgs]:
-            d.free()
+            if d is not None:
+                d.free()
 
 
 def tx_leg(eng, wl, steps, warmup):
@@ -911,6 +916,7 @@ def main():
         legs["c3_rx_payload_fused"] = fused_leg(eng, wl, args.steps, 2)
         two = legs["payload_gather"]["kernels_us"] + (region_ms / args.steps * 1e3)
         legs["c3_rx_payload_fused"]["two_pass_us"] = round(two, 2)  # rx_burst_dev + payload_gather_dev
+        legs["c3_rx_payload_by_reference"] = fused_leg(eng, wl, args.steps, 2, by_reference=True)
         legs["tx_generate_dev"] = tx_leg(eng, wl, args.steps, 2)
         legs["c3_copy_inclusive"] = copy_inclusive_leg(eng, wl, max(3, args.steps // 4), 1, device)
         legs["c5_bidir_copy_inclusive"] = c5_leg(eng, frames, max(3, args.steps // 4), 1, device,

@@ -976,15 +976,33 @@ extern "C" int rxg_rx_burst_dev(rxg_ctx *c, const rxg_dev_batch *b, void *stream
     return launch_bursts(c, b->frames, &one, 1, b->rec_kind, stream, "rxg_rx_burst_dev");
 }
 
+static int check_slots(const rxg_payload_slots *p, uint32_t n, const char *who)
+{
+    if (n && !p->msgs) return fail(-EINVAL, "%s: NULL msgs", who);
+    if ((uintptr_t)p->arena & 63u) return fail(-EINVAL, "%s: arena not 64-byte aligned", who);
+    if ((uintptr_t)p->msgs & 15u) return fail(-EINVAL, "%s: msgs not 16-byte aligned", who);
+    return 0;
+}
+
 extern "C" int rxg_rx_burst_payload_dev(rxg_ctx *c, const rxg_dev_batch *b, const rxg_payload_slots *p, void *stream)
 {
     if (!c || !b || !p) return fail(-EINVAL, "rxg_rx_burst_payload_dev: NULL argument");
-    if (b->n && (!b->frames || !b->off64 || !b->len || !b->out || !p->arena || !p->msgs))
+    if (b->n && (!b->frames || !b->off64 || !b->len || !b->out))
         return fail(-EINVAL, "rxg_rx_burst_payload_dev: NULL device pointer");
-    if ((uintptr_t)p->arena & 63u) return fail(-EINVAL, "rxg_rx_burst_payload_dev: arena not 64-byte aligned");
-    if ((uintptr_t)p->msgs & 15u) return fail(-EINVAL, "rxg_rx_burst_payload_dev: msgs not 16-byte aligned");
+    if (int rc = check_slots(p, b->n, "rxg_rx_burst_payload_dev")) return rc;
     const rxg_dev_burst one{b->off64, b->len, b->n, 0u, b->out};
     return launch_bursts(c, b->frames, &one, 1, b->rec_kind, stream, "rxg_rx_burst_payload_dev", 0u, p);
+}
+
+extern "C" int rxg_rx_burst_strided_payload_dev(rxg_ctx *c, const void *frames, uint32_t stride64,
+                                                const rxg_dev_strided_burst *b, uint32_t rec_kind,
+                                                const rxg_payload_slots *p, void *stream)
+{
+    if (!c || !b || !p) return fail(-EINVAL, "rxg_rx_burst_strided_payload_dev: NULL argument");
+    if (!stride64) return fail(-EINVAL, "rxg_rx_burst_strided_payload_dev: stride64 0");
+    if (int rc = check_slots(p, b->n, "rxg_rx_burst_strided_payload_dev")) return rc;
+    const rxg_dev_burst one{nullptr, b->len, b->n, b->slot0, b->out};
+    return launch_bursts(c, frames, &one, 1, rec_kind, stream, "rxg_rx_burst_strided_payload_dev", stride64, p);
 }
 
 extern "C" int rxg_rx_bursts_dev(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k,

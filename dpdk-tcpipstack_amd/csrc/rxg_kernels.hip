@@ -156,7 +156,7 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     }
     const bool strided = L.stride64 != 0u;
     if (L.pay_msgs) {  // the payload hand-off fused in (rxg_rx_burst_payload_dev): one burst
-        if (a.nbursts != 1 || !L.pay_arena) return hipErrorInvalidValue;
+        if (a.nbursts != 1) return hipErrorInvalidValue;  // (pay_arena NULL: by reference)
         const dim3 gb(g.blocks), tb(256);
         switch (L.mode) {
         case 8:

@@ -112,8 +112,9 @@ struct RxArgs {
     unsigned long long *counters;
     RxBurst b[kMaxBursts];
     // PAY kernels (rxg_rx_burst_payload_dev, one burst): the payload hand-off fused into the
-    // pass over the frames -- payload lines to pay_arena (the frame pool's geometry), one
-    // rxg_payload_msg per frame to pay_msgs.  (Last: the other fields keep their offsets.)
+    // pass over the frames -- payload lines to pay_arena (the frame pool's geometry; nullptr:
+    // by reference, nothing copied), one rxg_payload_msg per frame to pay_msgs.  (Last: the
+    // other fields keep their offsets.)
     uint8_t *pay_arena;
     rxg_payload_msg *pay_msgs;
 };
@@ -275,7 +276,9 @@ __device__ __forceinline__ void pay_lines_of(uint32_t span, uint32_t &lo, uint32
 
 // The frame's message (rxg_payload_msg): the payload at arena + 64*off + start, in place of
 // the frame's own bytes (the arena has the pool's geometry), or zeros.  f: its index in the
-// burst.  One 16-byte non-temporal store per lane.
+// burst.  One 16-byte non-temporal store per lane (staged in LDS with the records instead, the
+// fused C3 launch measured the same and C4 1.5 % faster, but the by-reference form 4 % slower
+// on the shorter ring it needs).
 __device__ __forceinline__ void pay_msg(const RxArgs &a, uint32_t f, bool valid, uint32_t off, uint32_t span)
 {
     if (!valid) return;
@@ -290,7 +293,7 @@ __device__ __forceinline__ void pay_msg(const RxArgs &a, uint32_t f, bool valid,
 // line, as loaded, when it carries a payload.
 __device__ __forceinline__ void pay_line_small(const RxArgs &a, uint32_t off, uint32_t span, const uint32_t (&q)[4][4])
 {
-    if (span == 0u) return;
+    if (span == 0u || a.pay_arena == nullptr) return;  // (no arena: hand-off by reference)
     uint8_t *dst = a.pay_arena + (size_t)off * 64u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) pay_store16<true>(dst + 16 * k, q[k]);
@@ -495,7 +498,7 @@ __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, ui
     F.h2 = h2;
     if constexpr (PAY) {  // every lane holds the header here (hdr_dword)
         const uint32_t span = pay_span(active, len, F.et, F.tl);
-        if (span != 0u) {
+        if (span != 0u && a.pay_arena != nullptr) {
             uint32_t lo, hi;
             pay_lines_of(span, lo, hi);
             uint8_t *dst = a.pay_arena + (size_t)off * 64u;
@@ -806,7 +809,7 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
         // lines, as loaded, at the same offset in the arena.  Whole lines (no partial-line
         // writes), no byte shift; the bytes written are the pool's own.
         const uint32_t span = lane_read(pay_span(leader, len, F.et, F.tl), gbase);
-        if (active && span != 0u) {
+        if (active && span != 0u && a.pay_arena != nullptr) {
             uint8_t *dst = a.pay_arena + (size_t)off * 64u;
 #pragma unroll
             for (int j = 0; j < NLOAD; ++j) {

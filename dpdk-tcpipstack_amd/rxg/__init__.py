@@ -299,6 +299,8 @@ def load_library(path: str = LIB_PATH):
         "rxg_replay_stats": (C.c_int, [vp, vp]),
         "rxg_payload_gather_dev": (C.c_int, [vp, C.POINTER(PayloadOut), vp]),
         "rxg_rx_burst_payload_dev": (C.c_int, [vp, C.POINTER(DevBatch), C.POINTER(PayloadSlots), vp]),
+        "rxg_rx_burst_strided_payload_dev": (C.c_int, [vp, vp, u32, C.POINTER(DevStridedBurst), u32,
+                                                       C.POINTER(PayloadSlots), vp]),
         "rxg_rcv_set": (C.c_int, [vp, i32, u32, u32]),
         "rxg_payload_take": (C.c_int, [vp, i32, u32, u32, C.POINTER(PayloadMsg)]),
         "rxg_synth_dev": (C.c_int, [vp, C.POINTER(SynthParams), vp, u64, vp, vp, vp,
@@ -634,6 +636,15 @@ class Engine:
         p = PayloadSlots(arena, msgs)
         _check(_lib.rxg_rx_burst_payload_dev(self.ctx, C.byref(b), C.byref(p), stream), "rxg_rx_burst_payload_dev")
 
+    def rx_burst_strided_payload_dev(self, frames: int, stride64: int, slot0: int, lens: int, n: int, out: int,
+                                     arena, msgs: int, rec_kind: int = REC16, stream=None):
+        """rxg_rx_burst_strided_payload_dev: one fixed-stride burst and its payload hand-off
+        (arena None: by reference)."""
+        b = DevStridedBurst(lens, n, slot0, out)
+        p = PayloadSlots(arena, msgs)
+        _check(_lib.rxg_rx_burst_strided_payload_dev(self.ctx, frames, stride64, C.byref(b), rec_kind, C.byref(p),
+                                                     stream), "rxg_rx_burst_strided_payload_dev")
+
     def rx_bursts_dev(self, frames: int, bursts, rec_kind: int = REC16, stream=None):
         """bursts: [(off64 ptr, len ptr, n, out ptr), ...] of one frame pool, one launch."""
         arr = (DevBurst * max(len(bursts), 1))(*[DevBurst(o, l, n, 0, out) for o, l, n, out in bursts])
@@ -735,11 +746,13 @@ class Engine:
         arena = da.download(np.uint8, min(arena_cap, used)) if arena_cap else np.zeros(0, np.uint8)
         return arena, msgs, used
 
-    def rx_burst_payload(self, frames, rec_kind: int = REC16, arena_fill: int | None = None):
+    def rx_burst_payload(self, frames, rec_kind: int = REC16, arena_fill: int | None = None,
+                         by_reference: bool = False):
         """Host frames through rxg_rx_burst_payload_dev (packed, uploaded): returns (records of
         rec_kind,
         payload arena as np.uint8 -- the pool's geometry -- , msgs, (arena, off64, lens) as
-        packed).  arena_fill: the payload arena's bytes before the call (None: zeros).  The
+        packed).  arena_fill: the payload arena's bytes before the call (None: zeros);
+        by_reference: no arena (the messages name the pool, which is then returned).  The
         device buffers live until the next call (the replay reads the batch, rxg_payload_take
         the messages)."""
         for d in getattr(self, "_pf_bufs", ()):
@@ -748,14 +761,18 @@ class Engine:
         n = len(frames)
         da, do, dl = self.to_device(arena), self.to_device(off), self.to_device(lens)
         dr, dm = self.alloc(max(n, 1) * rec_kind), self.alloc(max(n, 1) * 16)
-        dp = self.alloc(max(arena.nbytes, 64))
-        dp.upload(np.full(max(arena.nbytes, 64), 0 if arena_fill is None else arena_fill, dtype=np.uint8))
-        self._pf_bufs = (da, do, dl, dr, dm, dp)
-        self.rx_burst_payload_dev(da.ptr, do.ptr, dl.ptr, n, dr.ptr, dp.ptr, dm.ptr, rec_kind)
+        dp = None
+        if not by_reference:
+            dp = self.alloc(max(arena.nbytes, 64))
+            dp.upload(np.full(max(arena.nbytes, 64), 0 if arena_fill is None else arena_fill, dtype=np.uint8))
+        self._pf_bufs = tuple(d for d in (da, do, dl, dr, dm, dp) if d is not None)
+        self.rx_burst_payload_dev(da.ptr, do.ptr, dl.ptr, n, dr.ptr, dp.ptr if dp else None, dm.ptr, rec_kind)
         self.sync()
         recs = dr.download(rec_dtype(rec_kind), n)  # as the kernel wrote them (rec8_expand for REC8)
         msgs = dm.download(PAYLOAD_MSG_DTYPE, n) if n else np.zeros(0, PAYLOAD_MSG_DTYPE)
-        return recs, dp.download(np.uint8, arena.nbytes), msgs, (arena, off, lens)
+        # by reference the payloads are read from the pool itself (the uploaded batch)
+        pay = da.download(np.uint8, arena.nbytes) if by_reference else dp.download(np.uint8, arena.nbytes)
+        return recs, pay, msgs, (arena, off, lens)
 
     def rcv_set(self, idx: int, cur_seq: int, pairs_pending: bool):
         _check(_lib.rxg_rcv_set(self.ctx, idx, cur_seq & 0xFFFFFFFF, int(bool(pairs_pending))),

@@ -607,13 +607,22 @@ int rxg_payload_gather_dev(rxg_ctx *ctx, const rxg_payload_out *o, void *stream)
    the same offsets from `arena` (start = 34 + data_off*4), and msgs[i].arena_off = 64*off64[i]
    + start (not 16-byte aligned); other frames' lines are not written.  `arena` must hold
    64*(max off64[i]) + len rounded up to 64 bytes, and be 64-byte aligned; msgs 16-byte
-   aligned.  rxg_payload_take then answers from these messages, as after a gather.
-   Asynchronous on `stream`. */
+   aligned (128-byte alignment measured 8 % faster than 64).  arena NULL: the hand-off by
+   reference -- nothing is copied, each message names its payload in the frame pool itself
+   (arena_off from `frames`), for a stack that keeps the pool's buffers until the socket side
+   has consumed the messages (the reference's planned zero-copy path, currentstatus:9).
+   rxg_payload_take then answers from these messages, as after a gather.  Asynchronous on
+   `stream`. */
 typedef struct rxg_payload_slots {
-    void *arena;            /* dev: the pool's geometry (see above)               */
+    void *arena;            /* dev: the pool's geometry (see above), or NULL         */
     rxg_payload_msg *msgs;  /* dev, b->n messages                                   */
 } rxg_payload_slots;
 int rxg_rx_burst_payload_dev(rxg_ctx *ctx, const rxg_dev_batch *b, const rxg_payload_slots *p, void *stream);
+/* The same for one fixed-stride burst (rxg_rx_bursts_strided_dev's frame placement: frame i at
+   64-byte slot b->slot0 + i * stride64 of the pool, msgs[i].arena_off = 64 * that slot + start). */
+int rxg_rx_burst_strided_payload_dev(rxg_ctx *ctx, const void *frames, uint32_t stride64,
+                                     const rxg_dev_strided_burst *b, uint32_t rec_kind,
+                                     const rxg_payload_slots *p, void *stream);
 
 /* Receive-window mirror: ReceiveWindow.CurrentSequenceNumber of tcbs[idx] and whether its
    SeqPairs list is non-empty (tcp_windows.h:37-44).  The stack calls it wherever it

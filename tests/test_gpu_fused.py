@@ -195,3 +195,79 @@ def test_fused_multiflow_exchange_equals_reference(engine, seed):
     assert got.log == ref.log and got.rows == ref.rows
     assert got.sent == ref.sent
     assert got.taken == ref.eligible and got.eligible == 0 and got.taken > 200
+
+
+@pytest.mark.parametrize("rec_kind", [rxg.REC16, rxg.REC8])
+def test_fused_by_reference(engine, rec_kind):
+    """arena NULL: nothing copied; the same records, counters and messages, each message
+    naming its payload in the frame pool itself (the payload bytes read from there)."""
+    rows, frames = pktgen.parity_set(12, 3000)
+    tcb, live = pktgen.table_arrays(rows)
+    engine.tcb_load(tcb, live)
+    engine.arp_disable()
+    engine.counters_reset()
+    recs, pool, msgs, (arena, off, lens) = engine.rx_burst_payload(frames, rec_kind, by_reference=True)
+    cnt = engine.counters()
+    exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+    want = exp["c"].tobytes() if rec_kind == rxg.REC16 else rxg.rec8_pack(exp["c"]).tobytes()
+    assert recs.tobytes() == want and np.array_equal(cnt, ecnt)
+    assert pool.tobytes() == arena.tobytes()  # the pool itself, untouched
+    e_msgs, pays = opl.slots(frames, exp["c"], off)
+    assert msgs.tobytes() == e_msgs.tobytes()
+    for i, p in enumerate(pays):
+        if p is not None:
+            o = int(msgs[i]["arena_off"])
+            assert pool[o:o + len(p)].tobytes() == p
+
+
+def test_fused_by_reference_multiflow_exchange(engine):
+    """The C1 stack end to end with the hand-off by reference: PushData takes every eligible
+    payload from the pool, and the socket rings equal the reference's."""
+    from test_gpu_payload import multiflow_bursts
+    bursts = multiflow_bursts(3)
+    ref = c1.drive_cpu(bursts)
+    got = c1.drive_rxg(engine, bursts, fused=True, by_reference=True)
+    assert got.rings == ref.rings and got.log == ref.log and got.sent == ref.sent
+    assert got.taken == ref.eligible and got.taken > 200
+
+
+@pytest.mark.parametrize("len_a,by_ref", [(1500, False), (64, False), (576, False), (1500, True)])
+def test_fused_strided_equals_list_form(engine, len_a, by_ref):
+    """rxg_rx_burst_strided_payload_dev (frame i at slot slot0 + i * stride64, no off64[]) against
+    rxg_rx_burst_payload_dev over the same frames through their offset list: same records,
+    counters, messages and payload lines; a burst starting mid-pool (slot0 > 0)."""
+    n, flows = 20000, 500
+    b = engine.synth(n=n, nflows=flows, len_a=len_a, seed=0x5EED00AA)
+    tcb, live = rxg.synthetic_tcb_table(flows)
+    engine.tcb_load(tcb, live)
+    engine.tcb_sync()
+    stride = (len_a + 63) // 64
+    k0 = 3000  # the burst: frames k0 .. n-1
+    m = n - k0
+    nb = b["arena_bytes"]
+    outs = []
+    for form in ("list", "stride"):
+        recs, msgs = engine.alloc(m * 16), engine.alloc(m * 16)
+        pa = None if by_ref else engine.alloc(nb)
+        if pa is not None:
+            pa.upload(np.full(nb, SENTINEL, dtype=np.uint8))
+        engine.counters_reset()
+        if form == "list":
+            engine.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr + 4 * k0, b["len"].ptr + 2 * k0, m, recs.ptr,
+                                        pa.ptr if pa else None, msgs.ptr, rxg.REC16)
+        else:
+            engine.rx_burst_strided_payload_dev(b["arena"].ptr, stride, k0 * stride, b["len"].ptr + 2 * k0, m,
+                                                recs.ptr, pa.ptr if pa else None, msgs.ptr, rxg.REC16)
+        engine.sync()
+        outs.append((recs.download(np.uint8, m * 16).tobytes(), engine.counters().tolist(),
+                     msgs.download(rxg.PAYLOAD_MSG_DTYPE, m), pa.download(np.uint8, nb).tobytes() if pa else None))
+        for d in (recs, msgs, pa):
+            if d is not None:
+                d.free()
+    (r1, c1_, m1, a1), (r2, c2_, m2, a2) = outs
+    assert r1 == r2 and c1_ == c2_ and m1.tobytes() == m2.tobytes() and a1 == a2
+    off = b["off64"].download(np.uint32, n)[k0:].astype(np.uint64)
+    assert (m1["arena_off"] == off * 64 + 54).all() and (m1["len"] == len_a - 54).all()
+    for d in b.values():
+        if isinstance(d, rxg.DevArray):
+            d.free()
