@@ -13,7 +13,7 @@
 #include "rxg_kernels.h"
 #include "rxg_mirror.h"
 
-#include "rxg_rx.h"
+#include "rxg_rx_server.h"
 
 namespace rxg {
 

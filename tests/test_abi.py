@@ -262,7 +262,7 @@ def test_kernel_source_has_no_experiment_branches():
     scaffolding: no RXG_EXPERIMENTS blocks, no STRIP / ablation / stamp bits, and rx_body
     takes at most 6 template parameters."""
     csrc = os.path.join(ROOT, "dpdk-tcpipstack_amd", "csrc")
-    for f in ("rxg_kernels.hip", "rxg_rx.h"):
+    for f in ["rxg_kernels.hip"] + sorted(x for x in os.listdir(csrc) if x.startswith("rxg_rx")):
         src = open(os.path.join(csrc, f)).read()
         for word in ("RXG_EXPERIMENTS", "STRIP", "ABL", "SRVX", "kAbl", "abl_stamp"):
             assert word not in src, (f, word)
