@@ -26,7 +26,7 @@
 // handler creates their TCB inside the burst) with datalen > 0 and the payload inside the
 // frame.  The device does not decide whether the window takes the segment:
 // rxg_payload_take does, at replay time, against the receive-window mirror
-// (rxg_host.cpp), so gathering a segment that is never taken only costs its copy.
+// (rxg_replay.cpp), so gathering a segment that is never taken only costs its copy.
 //
 // Roofline: HBM, algorithmic bytes per frame = 2 x payload (read + write) + 16 (record)
 // + 16 (message descriptor).

@@ -2,7 +2,7 @@
 // §2.5) as a state machine over a Port, so its failure paths run in a CPU unit test
 // (tests/srvfsm_check.cpp) with a scripted device instead of a GPU.
 //
-// Port (rxg_host.cpp: the real mailbox, return block and stream):
+// Port (rxg_server.cpp: the real mailbox, return block and stream):
 //   unsigned long long done()    the number of the last request the server finished
 //   bool exited()                the kernel has left its loop (stop or idle)
 //   void write(q)                post request number q (mailbox words; the request body is

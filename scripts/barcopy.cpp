@@ -1,5 +1,5 @@
 // barcopy: how fast the rx thread can pack a host burst into fine-grained device memory
-// through the BAR (the latency-mode server's staging, rxg_host.cpp rxg_rx_burst): memcpy per
+// through the BAR (the latency-mode server's staging, rxg_server.cpp rxg_rx_burst): memcpy per
 // frame against AVX2 non-temporal 32-byte stores per frame, bursts of 32 / 256 frames of
 // 64 / 1500 bytes from mbuf-like sources (2 KiB apart, offset 128), each followed by an sfence.
 // build: hipcc -O2 -mavx2 barcopy.cpp -o build/barcopy
