@@ -7,7 +7,7 @@ chunk-granular / pipelined / 4-waves stores) were measured with it and removed a
 bench.py), the mean kernel time over K launches (one event pair around them), interleaved
 rounds, and a check that every variant writes the first one's records and messages; --shifts
 places the payload arena at other offsets from the pool.  One JSON line per measurement.
-  python scripts/fusedbench.py [--variants 0,0@512] [--rounds 3] [--steps 20] [--copy-ref]"""
+  python scripts/fusedbench.py [--variants 0,0@512] [--rounds 3] [--steps 20] [--copy-ref] [--by-ref]"""
 import argparse
 import json
 import os
@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--rec", type=int, default=8)
     ap.add_argument("--shifts", default="0", help="payload arena base offsets to try (bytes, multiples of 64)")
     ap.add_argument("--copy-ref", action="store_true", help="also time a device-to-device copy of 1.5 GiB")
+    ap.add_argument("--by-ref", action="store_true", help="the by-reference form (payload arena NULL: messages only)")
     args = ap.parse_args()
     # a variant "V@G" runs form V on a grid capped at G workgroups (rxg_config.max_blocks)
     variants = args.variants.split(",")
@@ -64,7 +65,7 @@ def main():
                 def launch(i):
                     b = bs[i % copies]
                     e.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, out.ptr,
-                                           arenas[i % copies].ptr + sh, msgs.ptr, rec)
+                                           0 if args.by_ref else arenas[i % copies].ptr + sh, msgs.ptr, rec)
                 for i in range(3):
                     launch(i)
                 e.sync()
@@ -84,7 +85,7 @@ def main():
                     ref = got
                 same = got[:2] == ref[:2]
                 delta = (arenas[0].ptr + sh) - bs[0]["arena"].ptr
-                print(json.dumps({"round": r, "workload": w, "variant": v, "arena_shift": sh,
+                print(json.dumps({"round": r, "workload": w, "variant": v, "by_ref": args.by_ref, "arena_shift": sh,
                                   "arena_minus_pool": delta, "kernel_us": round(us, 2),
                                   "same_records_and_msgs": bool(same)}), flush=True)
         for d in arenas + [out, msgs]:
