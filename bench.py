@@ -38,17 +38,18 @@ TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.jso
                  ("c2_64B_1flow", 1 << 20, 16): "profiles/r02/c2/traffic.json",
                  ("c4_imix_64Kflows", 1 << 20, 16): "profiles/r02/c4/traffic.json",
                  ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r02/c2multi/traffic.json",
-                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r04/c3/traffic.json",
-                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r04/c2/traffic.json",
-                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r04/c4/traffic.json",
-                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r04/c2multi/traffic.json",
+                 # the record-8 legs re-profiled on this tree (REC=8 scripts/gpu_prof.sh, scripts/runs/r05/r05o.sh)
+                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r05/c3/traffic.json",
+                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r05/c2/traffic.json",
+                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r05/c4/traffic.json",
+                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r05/c2multi/traffic.json",
                  # the 8(f) kernels over the headline's C3 batch (REC=8 scripts/gpu_prof.sh r05a tx3 pg3, this tree)
                  ("tx_generate_dev", 1 << 20, 8): "profiles/r05/tx3/traffic.json",
                  ("payload_gather", 1 << 20, 8): "profiles/r05/pg3/traffic.json",
                  ("c3_rx_payload_fused", 1 << 20, 8): "profiles/r05/pf3/traffic.json",
-                 # round 4: the fixed-stride forms (rxg_rx_bursts_strided_dev), scripts/gpu_prof.sh c2s c2multis
-                 ("c2_64B_1flow_strided", 1 << 20, 8): "profiles/r04/c2s/traffic.json",
-                 ("c2_64B_1flow_multiburst_strided", 1 << 20, 8): "profiles/r04/c2multis/traffic.json"}
+                 # the fixed-stride forms (rxg_rx_bursts_strided_dev), scripts/gpu_prof.sh c2s c2multis
+                 ("c2_64B_1flow_strided", 1 << 20, 8): "profiles/r05/c2s/traffic.json",
+                 ("c2_64B_1flow_multiburst_strided", 1 << 20, 8): "profiles/r05/c2multis/traffic.json"}
 
 
 def traffic_of(name, n, rec):

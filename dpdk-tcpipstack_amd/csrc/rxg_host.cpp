@@ -701,8 +701,9 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
             L.pay_msgs = pay->msgs;
         }
         L.counters = c->nocount ? nullptr : c->counters;
-        L.max_blocks = c->max_blocks ? c->max_blocks : pay ? c->grid_pay : (rec_kind == RXG_REC48 ? c->grid_rec48
-                                                        : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
+        // (the by-reference hand-off writes no payload: the record kind's occupancy grid)
+        L.max_blocks = c->max_blocks ? c->max_blocks : pay && pay->arena ? c->grid_pay
+                     : (rec_kind == RXG_REC48 ? c->grid_rec48 : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
         if (L.max_blocks == 0) L.max_blocks = 1024;
         HIP_OK(rx_launch(c, L, st));
     }

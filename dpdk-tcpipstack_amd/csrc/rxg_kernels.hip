@@ -144,6 +144,16 @@ static void launch_mode(const RxArgs &a, const RxGrid &g, hipStream_t st)
         hipLaunchKernelGGL((rx_kernel<MODE, DESC, false, false>), dim3(g.blocks), dim3(256), 0, st, a);
 }
 
+// The fused payload hand-off's kernels (one burst; offset list or fixed stride).
+template <int MODE, int PAY>
+static void launch_pay(const RxArgs &a, const RxGrid &g, bool strided, hipStream_t st)
+{
+    if (strided)
+        hipLaunchKernelGGL((rx_kernel<MODE, kDescStride, false, false, PAY>), dim3(g.blocks), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((rx_kernel<MODE, kDescList, false, false, PAY>), dim3(g.blocks), dim3(256), 0, st, a);
+}
+
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
 {
     RxArgs a;
@@ -156,21 +166,12 @@ hipError_t launch_rx(const LaunchRx &L, hipStream_t st)
     }
     const bool strided = L.stride64 != 0u;
     if (L.pay_msgs) {  // the payload hand-off fused in (rxg_rx_burst_payload_dev): one burst
-        if (a.nbursts != 1) return hipErrorInvalidValue;  // (pay_arena NULL: by reference)
-        const dim3 gb(g.blocks), tb(256);
+        if (a.nbursts != 1) return hipErrorInvalidValue;
+        const bool copy = L.pay_arena != nullptr;  // (NULL: by reference, messages only)
         switch (L.mode) {
-        case 8:
-            if (strided) hipLaunchKernelGGL((rx_kernel<8, kDescStride, false, false, true>), gb, tb, 0, st, a);
-            else hipLaunchKernelGGL((rx_kernel<8, kDescList, false, false, true>), gb, tb, 0, st, a);
-            break;
-        case 16:
-            if (strided) hipLaunchKernelGGL((rx_kernel<16, kDescStride, false, false, true>), gb, tb, 0, st, a);
-            else hipLaunchKernelGGL((rx_kernel<16, kDescList, false, false, true>), gb, tb, 0, st, a);
-            break;
-        case 48:
-            if (strided) hipLaunchKernelGGL((rx_kernel<48, kDescStride, false, false, true>), gb, tb, 0, st, a);
-            else hipLaunchKernelGGL((rx_kernel<48, kDescList, false, false, true>), gb, tb, 0, st, a);
-            break;
+        case 8: copy ? launch_pay<8, kPayCopy>(a, g, strided, st) : launch_pay<8, kPayRef>(a, g, strided, st); break;
+        case 16: copy ? launch_pay<16, kPayCopy>(a, g, strided, st) : launch_pay<16, kPayRef>(a, g, strided, st); break;
+        case 48: copy ? launch_pay<48, kPayCopy>(a, g, strided, st) : launch_pay<48, kPayRef>(a, g, strided, st); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

@@ -107,14 +107,28 @@ __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane,
 // (measured: 271 µs with 1 KiB stored per slice as it completes, 244 µs staged and
 // written at the end, 243 µs with no record stores at all), HBM read/write turnarounds.
 // Record bytes of one slice (64 frames) in the ring, in uint4: REC8 512 B, REC16 1 KiB,
-// REC48 3 KiB.
-constexpr int ring_slot_u4(int mode) { return mode * 64 / 16; }
+// REC48 3 KiB; MSG (the by-reference payload hand-off) adds the slice's 64 messages, 1 KiB.
+constexpr int ring_slot_u4(int mode, bool msg = false) { return mode * 64 / 16 + (msg ? 64 : 0); }
 
-template <int MODE, int RS>
+template <bool NTS>
+__device__ __forceinline__ void ring_store16(uint4 *p, const uint4 &q)
+{
+    if constexpr (NTS) {
+        typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+        v4 v;
+        v.x = q.x; v.y = q.y; v.z = q.z; v.w = q.w;
+        __builtin_nontemporal_store(v, reinterpret_cast<v4 *>(p));
+    } else {
+        *p = q;
+    }
+}
+
+template <int MODE, int RS, bool MSG = false>
 struct RecRing {
     static constexpr int kQ = MODE / 16;  // uint4 per record (REC16 / REC48)
-    static constexpr int kSlot = ring_slot_u4(MODE);
-    uint4 (*img)[kSlot];                  // [RS][kSlot]: the slice's records, contiguous
+    static constexpr int kRec = ring_slot_u4(MODE);
+    static constexpr int kSlot = ring_slot_u4(MODE, MSG);
+    uint4 (*img)[kSlot];                  // [RS][kSlot]: the slice's records, contiguous (MSG: then its messages)
     uint32_t *base;                       // [RS]: the slot's launch slice
     uint32_t n = 0;                       // slots in use (wave-uniform)
 
@@ -129,6 +143,9 @@ struct RecRing {
         if (n + need > (uint32_t)RS) flush<NTS>(a, lane, bc);
         return reinterpret_cast<uint32_t *>(img[n]);
     }
+
+    // MSG: this lane's message for the slot put() fills next (call first: put advances)
+    __device__ __forceinline__ void put_msg(int lane, const uint4 &m) { img[n][kRec + lane] = m; }
 
     __device__ __forceinline__ void put(uint32_t slice, int lane, const Rec &r)
     {
@@ -147,7 +164,8 @@ struct RecRing {
     }
 
     // Writes out every staged slice: uint4 k*64 + lane of each slot, so a wave-instruction
-    // stores 1 KiB contiguously.  Records of frames >= n_frames are not written.  NTS:
+    // stores 1 KiB contiguously (MSG: then the slice's messages, one burst per launch, 1 KiB
+    // per instruction).  Records of frames >= n_frames are not written.  NTS:
     // non-temporal stores, used when the small-frame path flushes (C2 0.8-6 % faster across
     // boxes; the 1 500 B path keeps plain stores: 247.5 vs 250.5 us with non-temporal ones).
     template <bool NTS = false, typename BC>
@@ -161,6 +179,12 @@ struct RecRing {
             const uint32_t kb = bc.of(a, sl);
             const uint32_t f0 = (sl - bc.slice0_of(a, kb)) * 64u;  // first frame of the slice in its burst
             const uint32_t nb = bc.n_of(a, kb);
+            if constexpr (MSG) {  // the slice's messages (one burst per launch)
+                if (f0 + (uint32_t)lane < nb) {
+                    const uint4 q = img[i][kRec + lane];
+                    ring_store16<NTS>(reinterpret_cast<uint4 *>(a.pay_msgs) + f0 + lane, q);
+                }
+            }
             if constexpr (MODE == 8) {  // 64 lanes x 8 B: 512 B contiguous per instruction
                 uint2 *d8 = reinterpret_cast<uint2 *>(bc.out_of(a, kb) + (size_t)f0 * 8u);
                 if (f0 + (uint32_t)lane < nb) {
@@ -200,10 +224,10 @@ struct RecRing {
 
 // One all-small slice s whose frames are in flight in vb[P]; prefetches slice s + nwaves
 // into vb[1-P] when it is all-small too (and returns true: the caller continues the run).
-template <int P, int MODE, int DESC, bool VWALK, int RS, bool PAY, typename BC>
+template <int P, int MODE, int DESC, bool VWALK, int RS, int PAY, typename BC>
 __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &s, uint32_t nslices,
                                            uint32_t nwaves, uint32_t &c_off, uint32_t &c_len, uint32_t &n_off,
-                                           uint32_t &n_len, uint4 (&vb)[2][4], RecRing<MODE, RS> &ring,
+                                           uint32_t &n_len, uint4 (&vb)[2][4], RecRing<MODE, RS, PAY == kPayRef> &ring,
                                            WaveCounters &wc, Rec &rec, FlowCache &fc, unsigned long long &bytes,
                                            BC &bc)
 {
@@ -223,10 +247,15 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     // more than the frames did
     const bool nxt = s1 < nslices && slice_frames(a, uniform(s1), bc) == 64u && __ballot(n_len <= 64u) == ~0ull;
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
+    uint4 msg = make_uint4(0u, 0u, 0u, 0u);  // (kPayRef: staged with the record)
     if constexpr (PAY) {  // (one burst per PAY launch: frame s * 64 + lane)
         const uint32_t span = pay_span(valid, c_len, F.et, F.tl);
-        pay_line_small(a, c_off, span, d);
-        pay_msg(a, s * 64u + (uint32_t)lane, valid, c_off, span);
+        if constexpr (PAY == kPayCopy) {
+            pay_line_small(a, c_off, span, d);
+            pay_msg(a, s * 64u + (uint32_t)lane, valid, c_off, span);
+        } else {
+            msg = pay_msg_of(c_off, span);
+        }
     }
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
@@ -246,6 +275,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     classify_finish<MODE, VWALK>(a, valid, c_len, F, PO, wc, rec, fc, cached);
     bytes += valid ? c_len : 0u;
     if (ring.n == RS) ring.template flush<true>(a, lane, bc);
+    if constexpr (PAY == kPayRef) ring.put_msg(lane, msg);
     ring.put(s, lane, rec);
     s = s1;
     c_off = n_off; c_len = n_len;
@@ -260,11 +290,11 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
 // ahead and are issued before the frames (vmcnt retires in order: the next step's check of
 // them then waits for nothing younger).  pend: s + nwaves's frames are in vb[1-P]; returns
 // whether the run continues with it.
-template <int P, int MODE, int DESC, bool VWALK, int RS, bool PAY, typename BC>
+template <int P, int MODE, int DESC, bool VWALK, int RS, int PAY, typename BC>
 __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t &s, uint32_t nslices,
                                             uint32_t nwaves, uint32_t &c_off, uint32_t &c_len, uint32_t &n_off,
                                             uint32_t &n_len, uint32_t &y_off, uint32_t &y_len, bool &pend,
-                                            uint4 (&vb)[2][4], RecRing<MODE, RS> &ring, WaveCounters &wc, Rec &rec,
+                                            uint4 (&vb)[2][4], RecRing<MODE, RS, PAY == kPayRef> &ring, WaveCounters &wc, Rec &rec,
                                             FlowCache &fc, unsigned long long &bytes, BC &bc)
 {
     const uint32_t s1 = s + nwaves, s2 = s + 2u * nwaves;
@@ -272,10 +302,15 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
     uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
     transpose_small_slice(vb[P], lane, sf, d);
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
+    uint4 msg = make_uint4(0u, 0u, 0u, 0u);  // (kPayRef: staged with the record)
     if constexpr (PAY) {
         const uint32_t span = pay_span(true, c_len, F.et, F.tl);
-        pay_line_small(a, c_off, span, d);
-        pay_msg(a, s * 64u + (uint32_t)lane, true, c_off, span);
+        if constexpr (PAY == kPayCopy) {
+            pay_line_small(a, c_off, span, d);
+            pay_msg(a, s * 64u + (uint32_t)lane, true, c_off, span);
+        } else {
+            msg = pay_msg_of(c_off, span);
+        }
     }
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
     const bool is_tcp = et == RXG_ETHER_TYPE_IPV4 && proto == RXG_IPPROTO_TCP;
@@ -288,6 +323,7 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
     classify_finish<MODE, VWALK>(a, true, c_len, F, PO, wc, rec, fc, cached);
     bytes += c_len;
     if (ring.n == RS) ring.template flush<true>(a, lane, bc);
+    if constexpr (PAY == kPayRef) ring.put_msg(lane, msg);
     ring.put(s, lane, rec);
     const bool cont = pend;
     pend = nxt2;
@@ -306,11 +342,12 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
 //   MULTI  several bursts of one frame pool per launch (BurstCursor)
 //   DEEP   runs of all-small slices prefetched two slices deep (small_step2); launch_rx picks
 //          it for launches of at least kDeepSlicesPerWave slices per wave
-//   PAY    the payload hand-off fused in (rxg_rx_burst_payload_dev: one burst, launched)
+//   PAY    the payload hand-off fused in (rxg_rx_burst_payload_dev: one burst, launched):
+//          kPayCopy with the payload lines copied, kPayRef by reference (messages only)
 //   SRV    the server's form: streaming-class rounds software-pipelined (a served burst's
 //          frame reads are latency-bound: 32 x 1500 B bursts 25.6-27.6 -> 22.2-23.2 us) and
 //          overflow walks with vector loads (VWALK, see sload_bucket)
-template <int MODE, int DESC, bool MULTI, bool DEEP, bool SRV, bool PAY = false>
+template <int MODE, int DESC, bool MULTI, bool DEEP, bool SRV, int PAY = kPayNone>
 __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
 {
     constexpr int NF = MODE == 48 ? NF48 : NF16;
@@ -320,8 +357,13 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     // small-slice transpose, NF x 256 B parked fields), so LDS per wave is the ring alone.
     // 3 workgroups per CU (LDS and, at ~145 VGPRs, registers).
     // (tx, MODE 0: 4 x 1 KiB, the class-0 transpose's scratch; no records)
-    constexpr int RS = MODE == 16 ? 11 : MODE == 48 ? 4 : MODE == 8 ? 22 : 4;
-    constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE);
+    // kPayRef (the by-reference hand-off): each slot also holds the slice's messages, in about
+    // the same LDS (REC8 7 slots of 1.5 KiB, REC16 5 of 2 KiB, REC48 3 of 4 KiB), so a flush
+    // writes as many bytes as without them.
+    constexpr bool MSG = PAY == kPayRef;
+    constexpr int RS = MSG ? (MODE == 16 ? 5 : MODE == 48 ? 3 : 7)
+                           : (MODE == 16 ? 11 : MODE == 48 ? 4 : MODE == 8 ? 22 : 4);
+    constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE, MSG);
     static_assert(MODE == 0 || (RS * kSlot * 16 >= 4096 + kSlot * 16 && RS * kSlot * 16 >= NF * 256 + 4096),
                   "ring too small for the scratch");
     __shared__ __attribute__((aligned(16))) uint4 s_rec[4][RS][kSlot];
@@ -335,7 +377,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
 #pragma unroll
     for (int k = 0; k < RXG_NCOUNTERS; ++k) wc.c[k] = 0u;
     unsigned long long bytes = 0ull;
-    RecRing<MODE == 0 ? 16 : MODE, RS> ring;
+    RecRing<MODE == 0 ? 16 : MODE, RS, MSG> ring;
     ring.img = s_rec[wid];
     ring.base = s_recf[wid];
     Rec rec;
@@ -491,10 +533,13 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const Fields F = unpark_fields<MODE>(sf, lane);
-            if constexpr (PAY) pay_msg(a, s * 64u + (uint32_t)lane, valid, off, pay_span(valid, len, F.et, F.tl));
+            uint4 msg = make_uint4(0u, 0u, 0u, 0u);  // (kPayRef: staged with the record)
+            if constexpr (PAY == kPayCopy) pay_msg(a, s * 64u + (uint32_t)lane, valid, off, pay_span(valid, len, F.et, F.tl));
+            if constexpr (PAY == kPayRef) msg = pay_msg_of(off, pay_span(valid, len, F.et, F.tl));
             classify_store<MODE, SRV>(a, valid, len, F, wc, rec, fcache, sf + NF * 64);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
             if (ring.n == RS) ring.flush(a, lane, bc);
+            if constexpr (PAY == kPayRef) ring.put_msg(lane, msg);
             ring.put(s, lane, rec);
         }
         s += nwaves;
@@ -547,7 +592,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
 
 // One launch per batch (rxg_rx_burst_dev / _bursts_dev / _strided_dev, the replay's
 // re-classification, rxg_tx_cksum_dev): a grid-stride over the launch's slices.
-template <int MODE, int DESC, bool MULTI, bool DEEP, bool PAY = false>
+template <int MODE, int DESC, bool MULTI, bool DEEP, int PAY = kPayNone>
 __global__ __launch_bounds__(256, 1) void rx_kernel(RxArgs a)
 {
     static_assert(!(PAY && (MULTI || MODE == 0 || DESC == kDescSel)), "PAY: one receive burst");

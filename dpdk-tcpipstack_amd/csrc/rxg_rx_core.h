@@ -199,6 +199,10 @@ struct Rec {
 };
 
 // ------------------------------------------------- fused payload hand-off (PAY) ---
+// The PAY template argument: no hand-off, the hand-off with its payload lines copied to the
+// arena, or by reference (messages only; rxg_payload_slots.arena NULL).
+enum : int { kPayNone = 0, kPayCopy = 1, kPayRef = 2 };
+
 // The payload a frame hands to the socket ring (the candidates of
 // rxg_payload_gather_dev, oracle/payload.py): a TCP segment (ether_type IPv4, proto 6: the
 // verdicts DISPATCH / RST_NOPCB / RST_LISTEN_NONSYN) of at least 54 bytes, datalen =
@@ -256,17 +260,24 @@ __device__ __forceinline__ void pay_lines_of(uint32_t span, uint32_t &lo, uint32
 }
 
 // The frame's message (rxg_payload_msg): the payload at arena + 64*off + start, in place of
-// the frame's own bytes (the arena has the pool's geometry), or zeros.  f: its index in the
-// burst.  One 16-byte non-temporal store per lane (staged in LDS with the records instead, the
-// fused C3 launch measured the same and C4 1.5 % faster, but the by-reference form 4 % slower
-// on the shorter ring it needs).
+// the frame's own bytes (the arena has the pool's geometry), or zeros.
+__device__ __forceinline__ uint4 pay_msg_of(uint32_t off, uint32_t span)
+{
+    const uint32_t dl = span & 0xFFFFu;
+    const uint64_t ao = span ? (uint64_t)off * 64u + (span >> 16) : 0ull;
+    return make_uint4((uint32_t)ao, (uint32_t)(ao >> 32), dl,
+                      span ? (RXG_PM_GATHERED | (dl >= 1000u ? RXG_PM_REF_OVERSIZE : 0u)) : 0u);
+}
+
+// The copy form's message store, f: the frame's index in the burst.  One 16-byte
+// non-temporal store per lane as the frame is classified (staged in LDS with the records
+// instead, the fused C3 launch measured the same and C4 1.5 % faster).  The
+// by-reference form stages its messages in the record ring (RecRing, MSG).
 __device__ __forceinline__ void pay_msg(const RxArgs &a, uint32_t f, bool valid, uint32_t off, uint32_t span)
 {
     if (!valid) return;
-    const uint32_t dl = span & 0xFFFFu;
-    const uint64_t ao = span ? (uint64_t)off * 64u + (span >> 16) : 0ull;
-    const uint32_t q[4] = {(uint32_t)ao, (uint32_t)(ao >> 32), dl,
-                           span ? (RXG_PM_GATHERED | (dl >= 1000u ? RXG_PM_REF_OVERSIZE : 0u)) : 0u};
+    const uint4 m = pay_msg_of(off, span);
+    const uint32_t q[4] = {m.x, m.y, m.z, m.w};
     nt_store16(reinterpret_cast<uint8_t *>(a.pay_msgs + f), q);
 }
 
@@ -274,7 +285,7 @@ __device__ __forceinline__ void pay_msg(const RxArgs &a, uint32_t f, bool valid,
 // line, as loaded, when it carries a payload.
 __device__ __forceinline__ void pay_line_small(const RxArgs &a, uint32_t off, uint32_t span, const uint32_t (&q)[4][4])
 {
-    if (span == 0u || a.pay_arena == nullptr) return;  // (no arena: hand-off by reference)
+    if (span == 0u) return;
     uint8_t *dst = a.pay_arena + (size_t)off * 64u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) pay_store16<true>(dst + 16 * k, q[k]);

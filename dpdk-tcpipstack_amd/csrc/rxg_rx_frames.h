@@ -84,11 +84,11 @@ __device__ __forceinline__ void load_chunks(const RxArgs &a, uint32_t off, uint3
     }
 }
 
-template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PAY = false>
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int PAY = kPayNone>
 __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                int lane, uint32_t (&d)[NLOAD][4]);
 
-template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PAY = false>
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int PAY = kPayNone>
 __device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                               int lane)
 {
@@ -100,7 +100,7 @@ __device__ __forceinline__ Fields frame_round(const RxArgs &a, uint32_t off, uin
 // Sums, header fields and (TX) checksum stores of the frames whose chunks are in d; PAY (the
 // jumbo class, frames over 2 KiB): the payload lines copied by the group, loaded again (the
 // chunks in d are only the first LPF * NLOAD).
-template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PAY>
+template <int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, int PAY>
 __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                int lane, uint32_t (&d)[NLOAD][4])
 {
@@ -204,9 +204,9 @@ __device__ __forceinline__ Fields frame_fields(const RxArgs &a, uint32_t off, ui
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
-    if constexpr (PAY) {  // every lane holds the header here (hdr_dword)
+    if constexpr (PAY == kPayCopy) {  // every lane holds the header here (hdr_dword)
         const uint32_t span = pay_span(active, len, F.et, F.tl);
-        if (span != 0u && a.pay_arena != nullptr) {
+        if (span != 0u) {
             uint32_t lo, hi;
             pay_lines_of(span, lo, hi);
             uint8_t *dst = a.pay_arena + (size_t)off * 64u;
@@ -380,7 +380,7 @@ __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32
 // The loads of one round of a streaming class: lane l of a group of LPF loads chunks
 // l, l + LPF, ... of its frame.  Inactive lanes: off = len = 0 (the arena's first SAFE bytes
 // exist: it holds a frame of this class).
-template <int C, int LPF, int NLOAD, bool NT, bool PAY = false>
+template <int C, int LPF, int NLOAD, bool NT, int PAY = kPayNone>
 __device__ __forceinline__ void round_load(const RxArgs &a, uint32_t off, uint32_t len, int lane,
                                            uint32_t (&d)[NLOAD][4])
 {
@@ -389,7 +389,7 @@ __device__ __forceinline__ void round_load(const RxArgs &a, uint32_t off, uint32
     const uint8_t *fp = a.frames + (size_t)off * 64u;
     // PAY: chunks up to the end of the frame's last 64-byte line are loaded as they are (that
     // line is readable, rxg_dev_batch): the payload's lines are written whole
-    const uint32_t lastc = len ? (PAY ? ((len + 63u) & ~63u) - 16u : ((len - 1u) & ~15u)) : 0u;
+    const uint32_t lastc = len ? (PAY == kPayCopy ? ((len + 63u) & ~63u) - 16u : ((len - 1u) & ~15u)) : 0u;
 #pragma unroll
     for (int j = 0; j < NLOAD; ++j) {
         const uint32_t o = (uint32_t)(gl + j * LPF) * 16u;
@@ -402,11 +402,11 @@ __device__ __forceinline__ void round_load(const RxArgs &a, uint32_t off, uint32
     }
 }
 
-template <int C, int LPF, int NLOAD, int MODE, bool NT, bool PAY = false>
+template <int C, int LPF, int NLOAD, int MODE, bool NT, int PAY = kPayNone>
 __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                       int lane, uint32_t (&d)[NLOAD][4]);
 
-template <int C, int LPF, int NLOAD, int MODE, bool NT, bool PAY = false>
+template <int C, int LPF, int NLOAD, int MODE, bool NT, int PAY = kPayNone>
 __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                    int lane)
 {
@@ -417,7 +417,7 @@ __device__ __forceinline__ Fields frame_round_fast(const RxArgs &a, uint32_t off
 
 // Sums, header fields and (tx) checksum stores of one round whose chunks are in d; PAY: the
 // payload lines written to the arena from the same registers.
-template <int C, int LPF, int NLOAD, int MODE, bool NT, bool PAY>
+template <int C, int LPF, int NLOAD, int MODE, bool NT, int PAY>
 __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t off, uint32_t len, bool active,
                                                       int lane, uint32_t (&d)[NLOAD][4])
 {
@@ -511,13 +511,13 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
     F.ack = (h10 >> 16) | (h11 << 16);
     F.h1 = h1;
     F.h2 = h2;
-    if constexpr (PAY) {
+    if constexpr (PAY == kPayCopy) {
         // The payload hand-off fused in: the leader's header gives the span (pay_span); every
         // lane of the group writes those of its chunks that fall in the payload's 64-byte
         // lines, as loaded, at the same offset in the arena.  Whole lines (no partial-line
         // writes), no byte shift; the bytes written are the pool's own.
         const uint32_t span = lane_read(pay_span(leader, len, F.et, F.tl), gbase);
-        if (active && span != 0u && a.pay_arena != nullptr) {
+        if (active && span != 0u) {
             uint8_t *dst = a.pay_arena + (size_t)off * 64u;
 #pragma unroll
             for (int j = 0; j < NLOAD; ++j) {
@@ -555,7 +555,7 @@ __device__ __forceinline__ void transpose_small_slice(const uint4 (&v)[4], int l
 
 // part / parts: this wave takes rounds part, part + parts, ... of the class (the server's
 // cooperative single slice, rx_body; 0 / 1 everywhere else).
-template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PIPE = false, bool PAY = false>
+template <int C, int LPF, int NLOAD, bool JUMBO, int MODE, bool NT, bool PIPE = false, int PAY = kPayNone>
 __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off, uint32_t len,
                                           int lane_in, uint32_t *sf, uint32_t part = 0u, uint32_t parts = 1u)
 {
@@ -659,7 +659,7 @@ __device__ __forceinline__ void run_class(const RxArgs &a, int cls, uint32_t off
             // (MODE 0, tx: no parked fields; the transpose uses the 4 KiB ring area itself)
             transpose_small_slice(v, rl, sf + (MODE == 0 ? 0 : MODE == 48 ? NF48 * 64 : NF16 * 64), d);
             F = fields_small<MODE>(const_cast<uint8_t *>(a.frames) + (size_t)koff * 64u, act ? klen : 0u, d);
-            if constexpr (PAY) pay_line_small(a, koff, pay_span(act, klen, F.et, F.tl), d);
+            if constexpr (PAY == kPayCopy) pay_line_small(a, koff, pay_span(act, klen, F.et, F.tl), d);
         } else if constexpr (LPF >= 2 && !JUMBO)
             F = frame_round_fast<C, LPF, NLOAD, MODE, NT, PAY>(a, act ? koff : 0u, act ? klen : 0u, act, rl);
         else

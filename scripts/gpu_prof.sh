@@ -3,7 +3,8 @@
 # FETCH_SIZE and WRITE_SIZE (separate runs: the TCC block holds 4 counters, FETCH_SIZE uses 3,
 # WRITE_SIZE 2), converted by scripts/pmc_traffic.py (gfx950: read = 2 x FETCH_SIZE).
 # Usage: [REC=8] scripts/gpu_prof.sh TAG WORKLOAD...   (c3 c2 c4 c2multi, tx3 tx4 = tx checksum
-# generate, pg3 pg4 = payload gather over C3 / C4, pf3 pf4 = rx + payload fused; REC: record kind, 16 default)
+# generate, pg3 pg4 = payload gather over C3 / C4, pf3 pf4 = rx + payload fused, pr3 pr4 = the
+# fused form by reference; REC: record kind, 16 default)
 set -u
 TAG=$1; shift
 REC=${REC:-16}
@@ -14,7 +15,8 @@ for W in "$@"; do
   case $W in  # the kernel the PMC passes count
     tx*) K="rx_kernel<0," ;;
     pg*) K="pg_gather" ;;
-    pf*) K="rx_kernel<$REC, 0, false, false, true>" ;;
+    pf*) K="rx_kernel<$REC, 0, false, false, 1>" ;;
+    pr*) K="rx_kernel<$REC, 0, false, false, 2>" ;;
     *)   K="rx_kernel<$REC," ;;
   esac
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $CMD > $O/trace.log 2>&1 || { echo "STOP trace $W"; exit 1; }

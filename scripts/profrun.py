@@ -20,7 +20,7 @@ WL = {"c3": (1500, 1000, 0, 2), "c2": (64, 1, 0, 16), "c4": (0, 65536, 1, 3)}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3", choices=sorted(WL) + ["c2s", "c2multi", "c2multis", "tx3", "tx4", "pg3", "pg4",
-                                                                      "pf3", "pf4"])
+                                                                      "pf3", "pf4", "pr3", "pr4"])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rec", type=int, default=16, choices=[8, 16, 48])
@@ -45,18 +45,18 @@ def main():
             eng.rx_bursts_dev(pool["arena"].ptr, bursts, rec)
         eng.sync()
         return
-    if args.workload[:2] == "pf":
+    if args.workload[:2] in ("pf", "pr"):
         # bench.py fused_leg: rxg_rx_burst_payload_dev over the C3 / C4 batches (rotating copies),
-        # each with a payload arena of the pool's size
+        # each with a payload arena of the pool's size ("pr": by reference, no arena)
         L, flows, mix, copies = WL["c3" if args.workload[2] == "3" else "c4"]
         bs = [eng.synth(n=n, nflows=flows, len_a=L or 1500, mix=mix, seed=0x5EED0001 + 17 * c) for c in range(copies)]
         eng.tcb_load(*rxg.synthetic_tcb_table(flows))
         out, msgs = eng.alloc(n * rec), eng.alloc(n * 16)
-        arenas = [eng.alloc(b["arena_bytes"]) for b in bs]
+        arenas = [eng.alloc(b["arena_bytes"]) for b in bs] if args.workload[:2] == "pf" else None
         for i in range(args.iters):
             b = bs[i % copies]
             eng.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, out.ptr,
-                                     arenas[i % copies].ptr, msgs.ptr, rec)
+                                     arenas[i % copies].ptr if arenas else 0, msgs.ptr, rec)
         eng.sync()
         return
     if args.workload[:2] in ("tx", "pg"):

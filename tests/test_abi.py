@@ -217,17 +217,18 @@ def _kernel_instantiations(path):
     (csrc/rxg_rx.h: rx_kernel<MODE, DESC, MULTI, DEEP, PAY>)."""
     data = open(path, "rb").read()
     return {tuple(int(x) for x in m) for m in
-            re.findall(rb"rx_kernelILi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELb(\d)EEEv", data)}
+            re.findall(rb"rx_kernelILi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELi(\d)EEEv", data)}
 
 
 # The product kernels: round 3's set (every record kind single / multi-burst, the two-deep
 # REC8 / REC16 forms, tx, the REC16 re-classification through a selection list), the
 # fixed-stride forms (DESC 2, rxg_rx_bursts_strided_dev), and round 5's fused payload
-# hand-off (PAY 1, rxg_rx_burst_payload_dev: one burst, every record kind, list or stride).
+# hand-off (rxg_rx_burst_payload_dev: one burst, every record kind, list or stride; PAY 1 with
+# the payload copied, PAY 2 by reference).
 PRODUCT_KERNELS = ({(m, d, mu, dp, 0) for m in (8, 16) for d in (0, 2) for mu in (0, 1) for dp in (0, 1)}
                    | {(48, d, mu, 0, 0) for d in (0, 2) for mu in (0, 1)}
                    | {(0, 0, 0, 0, 0), (16, 1, 0, 0, 0)}
-                   | {(m, d, 0, 0, 1) for m in (8, 16, 48) for d in (0, 2)})
+                   | {(m, d, 0, 0, p) for m in (8, 16, 48) for d in (0, 2) for p in (1, 2)})
 
 
 def test_product_library_has_no_experiment_switches():
