@@ -47,6 +47,7 @@ TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.jso
                  ("tx_generate_dev", 1 << 20, 8): "profiles/r05/tx3/traffic.json",
                  ("payload_gather", 1 << 20, 8): "profiles/r05/pg3/traffic.json",
                  ("c3_rx_payload_fused", 1 << 20, 8): "profiles/r05/pf3/traffic.json",
+                 ("c3_rx_payload_by_reference", 1 << 20, 8): "profiles/r05/pr3/traffic.json",
                  # the fixed-stride forms (rxg_rx_bursts_strided_dev), scripts/gpu_prof.sh c2s c2multis
                  ("c2_64B_1flow_strided", 1 << 20, 8): "profiles/r05/c2s/traffic.json",
                  ("c2_64B_1flow_multiburst_strided", 1 << 20, 8): "profiles/r05/c2multis/traffic.json"}
@@ -459,8 +460,8 @@ def fused_leg(eng, wl, steps, warmup, by_reference=False):
         c = eng.counters()
         m = msgs.download(rxg.PAYLOAD_MSG_DTYPE, wl.n)
         alg = wl.bytes_per_batch + (0 if by_reference else dl) + (16 + wl.rec) * wl.n
-        tb = (traffic_of("c3_rx_payload_fused", wl.n, wl.rec)[0]
-              if wl.name == "c3_1500B_1Kflows" and not by_reference else None)
+        tb = (traffic_of("c3_rx_payload_by_reference" if by_reference else "c3_rx_payload_fused", wl.n, wl.rec)[0]
+              if wl.name == "c3_1500B_1Kflows" else None)
         return {"kernel_us": round(k * 1e6, 2), "mpps": round(wl.n / k / 1e6, 1),
                 "payload_bytes": dl, "algorithmic_bytes_per_launch": alg,
                 "traffic_bytes_per_launch": tb,

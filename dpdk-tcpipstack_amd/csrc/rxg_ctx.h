@@ -65,6 +65,7 @@ struct rxg_ctx {
     uint32_t max_blocks = 0;        // rxg_config.max_blocks: grid cap (0 = occupancy grid)
     uint32_t grid_pay = 512;        // rxg_rx_burst_payload_dev's grid (set at init)
     uint32_t grid_rec8 = 0, grid_rec16 = 0, grid_rec48 = 0, grid_tx = 0;
+    uint32_t grid_ref8 = 0, grid_ref16 = 0, grid_ref48 = 0;  // the by-reference hand-off's
     // Experiment switches: only an experiment build (make experiments, -DRXG_EXPERIMENTS,
     // rxg/librxg_exp.so for scripts/kbench.py and pgbench.py) reads them from the
     // environment; in the product library they stay 0.

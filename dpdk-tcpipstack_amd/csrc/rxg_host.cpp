@@ -67,6 +67,9 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
         c->grid_rec16 = cus * (uint32_t)rx_blocks_per_cu(16);
         c->grid_rec48 = cus * (uint32_t)rx_blocks_per_cu(48);
         c->grid_tx = cus * (uint32_t)rx_blocks_per_cu(0);
+        c->grid_ref8 = cus * (uint32_t)rx_blocks_per_cu(8, true);
+        c->grid_ref16 = cus * (uint32_t)rx_blocks_per_cu(16, true);
+        c->grid_ref48 = cus * (uint32_t)rx_blocks_per_cu(48, true);
         // the fused burst + payload hand-off moves as many bytes out as in: 2 workgroups per CU
         // (8 waves) measured faster than the occupancy grid's 3 (C3 621 against 627 us, C4 174
         // against 177)
@@ -701,8 +704,9 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
             L.pay_msgs = pay->msgs;
         }
         L.counters = c->nocount ? nullptr : c->counters;
-        // (the by-reference hand-off writes no payload: the record kind's occupancy grid)
+        // (the by-reference hand-off writes no payload: its kernel's occupancy grid)
         L.max_blocks = c->max_blocks ? c->max_blocks : pay && pay->arena ? c->grid_pay
+                     : pay ? (rec_kind == RXG_REC48 ? c->grid_ref48 : rec_kind == RXG_REC8 ? c->grid_ref8 : c->grid_ref16)
                      : (rec_kind == RXG_REC48 ? c->grid_rec48 : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
         if (L.max_blocks == 0) L.max_blocks = 1024;
         HIP_OK(rx_launch(c, L, st));

@@ -159,8 +159,9 @@ hipError_t launch_server(const LaunchServer &L, hipStream_t st);
 // rxg_payload.hip: gather of the burst's candidate payloads (one launch + a memset)
 hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *tickets_used);
 uint32_t payload_blocks(uint32_t n);
-// resident 256-thread workgroups per CU of the production kernel of `mode`
-int rx_blocks_per_cu(int mode);
+// resident 256-thread workgroups per CU of the production kernel of `mode` (by_ref: the
+// by-reference payload hand-off's, whose record ring also stages the messages)
+int rx_blocks_per_cu(int mode, bool by_ref = false);
 hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);
 // off[i] = slot0 + i * stride64, i < n (a fixed-stride burst's offsets as a list)
 hipError_t launch_strided_offsets(uint32_t *off, uint32_t n, uint32_t slot0, uint32_t stride64, hipStream_t st);

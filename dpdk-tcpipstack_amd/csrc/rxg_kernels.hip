@@ -267,11 +267,17 @@ hipError_t launch_counters_add(unsigned long long *row, const CounterDelta &d, h
     return hipGetLastError();
 }
 
-int rx_blocks_per_cu(int mode)
+int rx_blocks_per_cu(int mode, bool by_ref)
 {
     int n = 0;
     hipError_t e;
-    if (mode == 8)
+    if (by_ref && mode == 8)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<8, kDescList, false, false, kPayRef>, 256, 0);
+    else if (by_ref && mode == 16)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<16, kDescList, false, false, kPayRef>, 256, 0);
+    else if (by_ref && mode == 48)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<48, kDescList, false, false, kPayRef>, 256, 0);
+    else if (mode == 8)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<8, kDescList, false, false>, 256, 0);
     else if (mode == 16)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rx_kernel<16, kDescList, false, false>, 256, 0);

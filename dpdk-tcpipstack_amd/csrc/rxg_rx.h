@@ -107,8 +107,10 @@ __device__ __forceinline__ void load_desc(const RxArgs &a, uint32_t s, int lane,
 // (measured: 271 µs with 1 KiB stored per slice as it completes, 244 µs staged and
 // written at the end, 243 µs with no record stores at all), HBM read/write turnarounds.
 // Record bytes of one slice (64 frames) in the ring, in uint4: REC8 512 B, REC16 1 KiB,
-// REC48 3 KiB; MSG (the by-reference payload hand-off) adds the slice's 64 messages, 1 KiB.
-constexpr int ring_slot_u4(int mode, bool msg = false) { return mode * 64 / 16 + (msg ? 64 : 0); }
+// REC48 3 KiB; MSG (the by-reference payload hand-off) adds the slice's 64 messages, 512 B
+// (8 bytes each: the frame's slot and payload span, expanded to rxg_payload_msg on the way
+// out, pay_msg_of).
+constexpr int ring_slot_u4(int mode, bool msg = false) { return mode * 64 / 16 + (msg ? 32 : 0); }
 
 template <bool NTS>
 __device__ __forceinline__ void ring_store16(uint4 *p, const uint4 &q)
@@ -144,8 +146,12 @@ struct RecRing {
         return reinterpret_cast<uint32_t *>(img[n]);
     }
 
-    // MSG: this lane's message for the slot put() fills next (call first: put advances)
-    __device__ __forceinline__ void put_msg(int lane, const uint4 &m) { img[n][kRec + lane] = m; }
+    // MSG: this lane's message (its frame's slot and payload span, pay_span) for the slot
+    // put() fills next (call first: put advances)
+    __device__ __forceinline__ void put_msg(int lane, uint32_t off, uint32_t span)
+    {
+        reinterpret_cast<uint2 *>(img[n] + kRec)[lane] = make_uint2(off, span);
+    }
 
     __device__ __forceinline__ void put(uint32_t slice, int lane, const Rec &r)
     {
@@ -181,8 +187,8 @@ struct RecRing {
             const uint32_t nb = bc.n_of(a, kb);
             if constexpr (MSG) {  // the slice's messages (one burst per launch)
                 if (f0 + (uint32_t)lane < nb) {
-                    const uint4 q = img[i][kRec + lane];
-                    ring_store16<NTS>(reinterpret_cast<uint4 *>(a.pay_msgs) + f0 + lane, q);
+                    const uint2 m = reinterpret_cast<const uint2 *>(img[i] + kRec)[lane];
+                    ring_store16<NTS>(reinterpret_cast<uint4 *>(a.pay_msgs) + f0 + lane, pay_msg_of(m.x, m.y));
                 }
             }
             if constexpr (MODE == 8) {  // 64 lanes x 8 B: 512 B contiguous per instruction
@@ -247,14 +253,13 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     // more than the frames did
     const bool nxt = s1 < nslices && slice_frames(a, uniform(s1), bc) == 64u && __ballot(n_len <= 64u) == ~0ull;
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
-    uint4 msg = make_uint4(0u, 0u, 0u, 0u);  // (kPayRef: staged with the record)
+    const uint32_t m_off = c_off;  // (kPayRef: the message, staged with the record)
+    uint32_t m_span = 0u;
     if constexpr (PAY) {  // (one burst per PAY launch: frame s * 64 + lane)
-        const uint32_t span = pay_span(valid, c_len, F.et, F.tl);
+        m_span = pay_span(valid, c_len, F.et, F.tl);
         if constexpr (PAY == kPayCopy) {
-            pay_line_small(a, c_off, span, d);
-            pay_msg(a, s * 64u + (uint32_t)lane, valid, c_off, span);
-        } else {
-            msg = pay_msg_of(c_off, span);
+            pay_line_small(a, c_off, m_span, d);
+            pay_msg(a, s * 64u + (uint32_t)lane, valid, c_off, m_span);
         }
     }
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
@@ -275,7 +280,7 @@ __device__ __forceinline__ bool small_step(const RxArgs &a, int lane, uint32_t &
     classify_finish<MODE, VWALK>(a, valid, c_len, F, PO, wc, rec, fc, cached);
     bytes += valid ? c_len : 0u;
     if (ring.n == RS) ring.template flush<true>(a, lane, bc);
-    if constexpr (PAY == kPayRef) ring.put_msg(lane, msg);
+    if constexpr (PAY == kPayRef) ring.put_msg(lane, m_off, m_span);
     ring.put(s, lane, rec);
     s = s1;
     c_off = n_off; c_len = n_len;
@@ -302,14 +307,13 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
     uint32_t *sf = ring.template scratch<true>(a, lane, 4096, bc);
     transpose_small_slice(vb[P], lane, sf, d);
     const Fields F = fields_small<MODE>(nullptr, c_len, d);
-    uint4 msg = make_uint4(0u, 0u, 0u, 0u);  // (kPayRef: staged with the record)
+    const uint32_t m_off = c_off;  // (kPayRef: the message, staged with the record)
+    uint32_t m_span = 0u;
     if constexpr (PAY) {
-        const uint32_t span = pay_span(true, c_len, F.et, F.tl);
+        m_span = pay_span(true, c_len, F.et, F.tl);
         if constexpr (PAY == kPayCopy) {
-            pay_line_small(a, c_off, span, d);
-            pay_msg(a, s * 64u + (uint32_t)lane, true, c_off, span);
-        } else {
-            msg = pay_msg_of(c_off, span);
+            pay_line_small(a, c_off, m_span, d);
+            pay_msg(a, s * 64u + (uint32_t)lane, true, c_off, m_span);
         }
     }
     const uint32_t et = F.et & 0xFFFFu, proto = (F.et >> 16) & 0xFFu;
@@ -323,7 +327,7 @@ __device__ __forceinline__ bool small_step2(const RxArgs &a, int lane, uint32_t 
     classify_finish<MODE, VWALK>(a, true, c_len, F, PO, wc, rec, fc, cached);
     bytes += c_len;
     if (ring.n == RS) ring.template flush<true>(a, lane, bc);
-    if constexpr (PAY == kPayRef) ring.put_msg(lane, msg);
+    if constexpr (PAY == kPayRef) ring.put_msg(lane, m_off, m_span);
     ring.put(s, lane, rec);
     const bool cont = pend;
     pend = nxt2;
@@ -357,11 +361,13 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     // small-slice transpose, NF x 256 B parked fields), so LDS per wave is the ring alone.
     // 3 workgroups per CU (LDS and, at ~145 VGPRs, registers).
     // (tx, MODE 0: 4 x 1 KiB, the class-0 transpose's scratch; no records)
-    // kPayRef (the by-reference hand-off): each slot also holds the slice's messages, in about
-    // the same LDS (REC8 7 slots of 1.5 KiB, REC16 5 of 2 KiB, REC48 3 of 4 KiB), so a flush
-    // writes as many bytes as without them.
+    // kPayRef (the by-reference hand-off): each slot also holds the slice's messages (512 B),
+    // REC8 12 slots of 1 KiB, REC16 8 of 1.5 KiB, REC48 3 of 3.5 KiB: up to 50 KB per
+    // workgroup, still 3 per CU (13 slots, 54 KB, left room for 2), so a wave's records and
+    // messages of a C3 launch (5-6 slices per wave) go out at its end, not between its frame
+    // loads.
     constexpr bool MSG = PAY == kPayRef;
-    constexpr int RS = MSG ? (MODE == 16 ? 5 : MODE == 48 ? 3 : 7)
+    constexpr int RS = MSG ? (MODE == 16 ? 8 : MODE == 48 ? 3 : 12)
                            : (MODE == 16 ? 11 : MODE == 48 ? 4 : MODE == 8 ? 22 : 4);
     constexpr int kSlot = ring_slot_u4(MODE == 0 ? 16 : MODE, MSG);
     static_assert(MODE == 0 || (RS * kSlot * 16 >= 4096 + kSlot * 16 && RS * kSlot * 16 >= NF * 256 + 4096),
@@ -533,13 +539,13 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const Fields F = unpark_fields<MODE>(sf, lane);
-            uint4 msg = make_uint4(0u, 0u, 0u, 0u);  // (kPayRef: staged with the record)
+            uint32_t m_span = 0u;  // (kPayRef: the message, staged with the record)
             if constexpr (PAY == kPayCopy) pay_msg(a, s * 64u + (uint32_t)lane, valid, off, pay_span(valid, len, F.et, F.tl));
-            if constexpr (PAY == kPayRef) msg = pay_msg_of(off, pay_span(valid, len, F.et, F.tl));
+            if constexpr (PAY == kPayRef) m_span = pay_span(valid, len, F.et, F.tl);
             classify_store<MODE, SRV>(a, valid, len, F, wc, rec, fcache, sf + NF * 64);
             __builtin_amdgcn_wave_barrier();  // phase B reads before the next slice's writes
             if (ring.n == RS) ring.flush(a, lane, bc);
-            if constexpr (PAY == kPayRef) ring.put_msg(lane, msg);
+            if constexpr (PAY == kPayRef) ring.put_msg(lane, off, m_span);
             ring.put(s, lane, rec);
         }
         s += nwaves;
