@@ -113,17 +113,20 @@ def test_fused_matches_burst_then_gather(engine):
         assert parena[a:a + L].tobytes() == g_arena[b:b + L].tobytes()
 
 
-def _fused_full(engine, n, flows, seed, mix, len_a=1500):
+def _fused_full(engine, n, flows, seed, mix, len_a=1500, by_reference=False):
     b = engine.synth(n=n, nflows=flows, len_a=len_a, mix=mix, seed=seed)
     tcb, live = rxg.synthetic_tcb_table(flows)
     engine.tcb_load(tcb, live)
     engine.tcb_sync()
     nb = b["arena_bytes"]
-    recs, msgs, parena = engine.alloc(n * 8), engine.alloc(n * 16), engine.alloc(nb)
-    parena.upload(np.full(nb, SENTINEL, dtype=np.uint8))
+    recs, msgs = engine.alloc(n * 8), engine.alloc(n * 16)
+    parena = None
+    if not by_reference:
+        parena = engine.alloc(nb)
+        parena.upload(np.full(nb, SENTINEL, dtype=np.uint8))
     engine.counters_reset()
-    engine.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, recs.ptr, parena.ptr, msgs.ptr,
-                                rxg.REC8)
+    engine.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, recs.ptr,
+                                parena.ptr if parena else None, msgs.ptr, rxg.REC8)
     engine.sync()
     return b, recs, msgs, parena
 
@@ -269,5 +272,37 @@ def test_fused_strided_equals_list_form(engine, len_a, by_ref):
     off = b["off64"].download(np.uint32, n)[k0:].astype(np.uint64)
     assert (m1["arena_off"] == off * 64 + 54).all() and (m1["len"] == len_a - 54).all()
     for d in b.values():
+        if isinstance(d, rxg.DevArray):
+            d.free()
+
+
+@pytest.mark.parametrize("mix", [0, 1])
+def test_fused_by_reference_full_size_property(engine, mix):
+    """The by-reference form at the BASELINE C3 / C4 sizes (2^20 frames: 5-6 slices per wave on
+    the occupancy grid, records and messages out of the ring at each wave's end): the
+    records and counters equal the copy form's, every message names its payload in the pool
+    (64 * off64 + 54, length len - 54), and the pool is untouched."""
+    n, flows, seed = 1 << 20, (1000, 65536)[mix], (0x5EED0001, 0x5EED0004)[mix]
+    b, recs, msgs, _ = _fused_full(engine, n, flows, seed, mix, by_reference=True)
+    cnt_ref = engine.counters()
+    r_ref = recs.download(np.uint8, n * 8)
+    m = msgs.download(rxg.PAYLOAD_MSG_DTYPE, n)
+    nb = b["arena_bytes"]
+    pool_sum = int(b["arena"].download(np.uint64, nb // 8).sum())  # (wrapping word sum)
+    off = b["off64"].download(np.uint32, n).astype(np.uint64)
+    lens = b["len"].download(np.uint16, n).astype(np.uint64)
+    assert (m["len"] == lens - 54).all() and (m["arena_off"] == off * 64 + 54).all()
+    want_flags = rxg.PM_GATHERED | np.where(lens - 54 >= 1000, rxg.PM_REF_OVERSIZE, 0)
+    assert (m["flags"] == want_flags).all()
+    # the copy form over the same batch: the same records and counters
+    parena = engine.alloc(nb)
+    engine.counters_reset()
+    engine.rx_burst_payload_dev(b["arena"].ptr, b["off64"].ptr, b["len"].ptr, n, recs.ptr, parena.ptr, msgs.ptr,
+                                rxg.REC8)
+    engine.sync()
+    assert np.array_equal(engine.counters(), cnt_ref)
+    assert recs.download(np.uint8, n * 8).tobytes() == r_ref.tobytes()
+    assert int(b["arena"].download(np.uint64, nb // 8).sum()) == pool_sum
+    for d in list(b.values()) + [recs, msgs, parena]:
         if isinstance(d, rxg.DevArray):
             d.free()

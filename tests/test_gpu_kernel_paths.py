@@ -166,3 +166,34 @@ def test_class_round_counts_tx(small_grid_engine):
     got = small_grid_engine.tx_arena(arena, off, lens)
     exp = oracle.tx_batch(arena, off, lens)
     assert got.tobytes() == exp.tobytes()
+
+
+@pytest.mark.parametrize("by_ref", [False, True])
+@pytest.mark.parametrize("rec_kind", [rxg.REC8, rxg.REC16, rxg.REC48])
+def test_many_slices_per_wave_fused(small_grid_engine, rec_kind, by_ref):
+    """The fused payload hand-off (rxg_rx_burst_payload_dev) over the same many-slices-per-wave
+    batches: the copy form, and the by-reference form whose record ring also stages the
+    messages, here flushing mid-stream from both the all-small and the class
+    path -- records, counters and every message bit-exact with the oracle, every payload's
+    bytes where its message points."""
+    from oracle import payload as opl
+    rows, frames = _batch(24)
+    tcb, live = pktgen.table_arrays(rows)
+    eng = small_grid_engine
+    eng.tcb_load(tcb, live)
+    eng.counters_reset()
+    recs, pay, msgs, (arena, off, lens) = eng.rx_burst_payload(frames, rec_kind, by_reference=by_ref)
+    cnt = eng.counters()
+    exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+    want = exp if rec_kind == rxg.REC48 else exp["c"] if rec_kind == rxg.REC16 else rxg.rec8_pack(exp["c"])
+    assert recs.tobytes() == want.tobytes()
+    assert np.array_equal(cnt, ecnt), (cnt, ecnt)
+    e_msgs, pays = opl.slots(frames, exp["c"], off)
+    for name in ("arena_off", "len", "flags"):
+        bad = np.nonzero(msgs[name] != e_msgs[name])[0]
+        assert len(bad) == 0, f"msgs.{name} differs at {len(bad)} frames, first {bad[:1]}"
+    assert (msgs["len"] > 0).sum() > 1000
+    for i, p in enumerate(pays):
+        if p is not None:
+            o = int(msgs[i]["arena_off"])
+            assert pay[o:o + len(p)].tobytes() == p, f"frame {i}: payload bytes differ"
