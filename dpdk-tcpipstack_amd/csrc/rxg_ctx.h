@@ -25,8 +25,6 @@
 #include "rxg_packpool.h"
 #include "rxg_srvfsm.h"
 
-using namespace rxg;
-
 // Everything below is internal to librxg.so: hidden, never exported.
 #pragma GCC visibility push(hidden)
 
@@ -81,7 +79,7 @@ struct rxg_ctx {
     rxg::MpscRing<rxg_tcb_op> posted{RXG_TCB_QUEUE_CAP};
 
     // host mirror of tcbs[0..ntcb) and the device words each write changes (rxg_mirror.h)
-    TcbMirror mir;
+    rxg::TcbMirror mir;
     bool dirty = true;  // mirror writes not on the device yet
 
     // device mirror
@@ -114,7 +112,7 @@ struct rxg_ctx {
     // the device for bursts running on caller streams, which can be long).
     static constexpr int kPatchBufs = 4;
     struct PatchBuf {
-        MirrorPatch *h = nullptr;
+        rxg::MirrorPatch *h = nullptr;
         uint32_t cap = 0;
         hipEvent_t ev = nullptr;
         bool set = false;
@@ -125,7 +123,7 @@ struct rxg_ctx {
 
     // mirror changes since the last clear, for rxg_rx_replay's re-classification
     uint64_t gen = 0;
-    std::vector<TupleKey> touched_keys;  // tuples (old and new) of changed slots
+    std::vector<rxg::TupleKey> touched_keys;  // tuples (old and new) of changed slots
     std::vector<int32_t> touched_listen; // dports whose LISTENING slots changed (pass 2)
     bool touched_all = false;            // whole table replaced
     bool touched_pass2 = false;          // min_null moved (the pass-2 NULL-slot flag)
@@ -148,7 +146,7 @@ struct rxg_ctx {
     uint32_t replay_cursor = 0;
     // writes absorbed by the replays of this launch's earlier bursts (they came after every
     // burst of the launch was classified)
-    std::vector<TupleKey> launch_keys;
+    std::vector<rxg::TupleKey> launch_keys;
     std::vector<int32_t> launch_listen;
     bool launch_all = false, launch_pass2 = false;
     const uint8_t *last_frames = nullptr;
@@ -180,7 +178,7 @@ struct rxg_ctx {
 
     // ARP mirror (host set + device open-addressing table, rxg_mirror.h)
     bool arp_enabled = false, arp_dirty = false;
-    ArpMirror arp;
+    rxg::ArpMirror arp;
     std::unordered_map<uint32_t, int> arp_since_burst;  // learned after the last burst
     DevBuf d_arp;
     uint32_t arp_mask = 0;
@@ -212,15 +210,15 @@ struct rxg_ctx {
     struct Server {
         bool on = false;        // configured (the kernel may have exited idle: relaunched on demand)
         rxg::SrvFsm<SrvPort> fsm;  // Down / Up / Failed (rxg_srvfsm.h)
-        SrvReq req{};           // the request SrvPort::write posts
+        rxg::SrvReq req{};      // the request SrvPort::write posts
         // its inline descriptors (kSrvInlineDesc): mailbox words 16-39, SrvMbox::ioff / ilen
-        alignas(16) unsigned long long idesc[kSrvPollWords - 16] = {};
+        alignas(16) unsigned long long idesc[rxg::kSrvPollWords - 16] = {};
         bool dev = false;       // arena / off / len in device memory (host writes only)
         bool mdev = false;      // mbox in device memory (large BAR, no RXG_SRV_HOST_MAILBOX)
         hipStream_t st = nullptr;
-        SrvMbox *mbox = nullptr;  // host-written words: seq, request, stop
-        SrvMbox *ret = nullptr;   // server-written words: done, exited (host memory; = mbox if !mdev)
-        SrvCtl *ctl = nullptr;
+        rxg::SrvMbox *mbox = nullptr;  // host-written words: seq, request, stop
+        rxg::SrvMbox *ret = nullptr;   // server-written words: done, exited (host memory; = mbox if !mdev)
+        rxg::SrvCtl *ctl = nullptr;
         uint8_t *arena = nullptr;
         uint32_t *off = nullptr;
         uint16_t *len = nullptr;
@@ -257,9 +255,9 @@ inline int ensure(DevBuf &b, size_t bytes)
 inline hipStream_t pick(rxg_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
 
 // The device tables as the kernels read them (DevTable, rxg_kernels.h).
-inline DevTable table_view(const rxg_ctx *c)
+inline rxg::DevTable table_view(const rxg_ctx *c)
 {
-    DevTable t;
+    rxg::DevTable t;
     t.buckets = (const uint4 *)c->buckets.p;
     t.listen = (const int32_t *)c->listen.p;
     t.bucket_mask = c->bucket_mask;
@@ -267,7 +265,7 @@ inline DevTable table_view(const rxg_ctx *c)
     t.min_null = c->dev_min_null;
     t.arp = (const uint4 *)c->d_arp.p;
     t.arp_mask = c->arp_enabled ? c->arp_mask : 0u;
-    t.arp_flags = c->arp_enabled ? (kArpOn | (c->arp.has_zero ? kArpZero : 0u)) : 0u;
+    t.arp_flags = c->arp_enabled ? (rxg::kArpOn | (c->arp.has_zero ? rxg::kArpZero : 0u)) : 0u;
     return t;
 }
 

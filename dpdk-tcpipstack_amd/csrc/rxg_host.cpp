@@ -23,6 +23,8 @@
 
 #include "rxg_ctx.h"
 
+using namespace rxg;
+
 static_assert(sizeof(rxg_rec16) == 16, "rxg_rec16 layout");
 static_assert(sizeof(rxg_rec48) == 48, "rxg_rec48 layout");
 static_assert(sizeof(rxg_tcb_tuple) == 20, "rxg_tcb_tuple layout");

@@ -12,6 +12,8 @@
 
 #include "rxg_ctx.h"
 
+using namespace rxg;
+
 extern "C" int rxg_ether_in(rxg_ctx *c, const rxg_handoff_ops *ops, void *mbuf, void *frame, uint16_t data_len)
 {
     if (!c || !ops || !frame) return fail(-EINVAL, "rxg_ether_in: NULL argument");

@@ -11,6 +11,8 @@
 
 #include "rxg_ctx.h"
 
+using namespace rxg;
+
 // ---------------------------------------------------------------- latency mode ---
 // (Re)launch the server kernel.  A previous kernel has left its loop (stop / idle) or none
 // ran (the state machine synchronised its stream first); the mailbox's stop, the return

@@ -10,6 +10,8 @@
 
 #include "rxg_ctx.h"
 
+using namespace rxg;
+
 // ---------------------------------------------------------------------- synthetic ---
 extern "C" uint64_t rxg_synth_arena_bytes(const rxg_synth_params *p)
 {
