@@ -120,6 +120,10 @@ struct rxg_ctx {
     int patch_next = 0;
 
     unsigned long long *counters = nullptr;
+    // the replays' counter corrections not yet on the device: added by the next mirror patch
+    // launch, or by counters_add at the next read / sync / rxg_counters_dev (flush_delta)
+    int64_t pend_delta[RXG_NCOUNTERS] = {};
+    bool pend = false;
 
     // mirror changes since the last clear, for rxg_rx_replay's re-classification
     uint64_t gen = 0;
@@ -275,6 +279,14 @@ void select_burst(rxg_ctx *c, uint32_t j);
 int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
                  const char *who, uint32_t stride64 = 0);
 int burst_offsets(rxg_ctx *c, hipStream_t st, const uint32_t **out);
+// the pending counter corrections (rxg_ctx::pend_delta) to the device, on c->stream
+int flush_delta(rxg_ctx *c);
+
+// the counter block's row of replay corrections (rxg.h RXG_COUNTER_ROWS: the last)
+inline unsigned long long *correction_row(rxg_ctx *c)
+{
+    return c->counters + (size_t)(RXG_COUNTER_ROWS - 1) * RXG_NCOUNTERS;
+}
 
 inline bool rec_kind_ok(uint32_t k) { return k == RXG_REC8 || k == RXG_REC16 || k == RXG_REC48; }
 

@@ -182,6 +182,7 @@ extern "C" int rxg_fini(rxg_ctx *c)
 extern "C" int rxg_sync(rxg_ctx *c)
 {
     if (!c) return fail(-EINVAL, "rxg_sync: ctx NULL");
+    if (int rc = flush_delta(c)) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -386,8 +387,15 @@ static int apply_patches(rxg_ctx *c, M &mirror)
     std::memcpy(pb.h, p.data(), p.size() * sizeof(MirrorPatch));
     int rc = wait_table_readers(c);
     if (rc) return rc;
+    // the last replay's counter corrections ride along (its table writes are why this runs)
+    CounterDelta d;
+    if (c->pend) std::memcpy(d.v, c->pend_delta, sizeof d.v);
     HIP_OK(launch_mirror_patch(pb.h, (uint32_t)p.size(), (uint4 *)c->buckets.p, (int32_t *)c->listen.p,
-                               (uint32_t *)c->d_arp.p, c->stream));
+                               (uint32_t *)c->d_arp.p, c->stream, c->pend ? correction_row(c) : nullptr, &d));
+    if (c->pend) {
+        std::memset(c->pend_delta, 0, sizeof c->pend_delta);
+        c->pend = false;
+    }
     HIP_OK(hipEventRecord(pb.ev, c->stream));
     pb.set = true;
     HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
@@ -831,10 +839,28 @@ extern "C" int rxg_tx_cksum_dev(rxg_ctx *c, const rxg_dev_tx_batch *b, void *str
 }
 
 // ----------------------------------------------------------------------- counters ---
+// The replay's counter corrections (rxg_rx_replay) wait on the host for the context's next
+// mirror patch launch, which a replay that changed any record always leads to (the change
+// came from a table write); a read, a sync or rxg_counters_dev adds them first.
+int flush_delta(rxg_ctx *c)
+{
+    if (!c->pend) return 0;
+    if (int rc = set_device(c)) return rc;
+    CounterDelta d;
+    std::memcpy(d.v, c->pend_delta, sizeof d.v);
+    HIP_OK(launch_counters_add(correction_row(c), d, c->stream));
+    std::memset(c->pend_delta, 0, sizeof c->pend_delta);
+    c->pend = false;
+    return 0;
+}
+
 extern "C" int rxg_counters_reset(rxg_ctx *c, void *stream)
 {
     if (!c) return fail(-EINVAL, "rxg_counters_reset: ctx NULL");
     if (int rc = set_device(c)) return rc;
+    // pending corrections belong to the bursts before the reset: zeroed with them
+    std::memset(c->pend_delta, 0, sizeof c->pend_delta);
+    c->pend = false;
     HIP_OK(hipMemsetAsync(c->counters, 0, kCounterBytes, pick(c, stream)));
     return 0;
 }
@@ -843,6 +869,7 @@ extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
 {
     if (!c || !out) return fail(-EINVAL, "rxg_counters_read: NULL argument");
     if (int rc = set_device(c)) return rc;
+    if (int rc = flush_delta(c)) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     std::vector<uint64_t> rows((size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS);
     HIP_OK(hipMemcpyAsync(rows.data(), c->counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
@@ -855,4 +882,9 @@ extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
     return 0;
 }
 
-extern "C" void *rxg_counters_dev(rxg_ctx *c) { return c ? (void *)c->counters : nullptr; }
+extern "C" void *rxg_counters_dev(rxg_ctx *c)
+{
+    if (!c) return nullptr;
+    (void)flush_delta(c);  // (on failure rxg_last_error says so; the block is still there)
+    return (void *)c->counters;
+}

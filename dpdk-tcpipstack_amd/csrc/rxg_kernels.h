@@ -173,7 +173,9 @@ struct CounterDelta {
 };
 hipError_t launch_counters_add(unsigned long long *row, const CounterDelta &d, hipStream_t st);
 
+// crow != nullptr: the launch also adds *delta to that counter row (the replay's pending
+// corrections, rxg_replay.cpp), saving their own launch
 hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets, int32_t *listen, uint32_t *arp,
-                               hipStream_t st);
+                               hipStream_t st, unsigned long long *crow = nullptr, const CounterDelta *delta = nullptr);
 
 }  // namespace rxg

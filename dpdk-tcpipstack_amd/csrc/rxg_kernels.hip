@@ -216,9 +216,12 @@ hipError_t launch_server(const LaunchServer &L, hipStream_t st)
 // patch; the host deduplicated them, so no two threads write the same word.  The patch list
 // is read straight from pinned host memory (a few hundred bytes per burst).
 __global__ __launch_bounds__(256) void mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets,
-                                                    int32_t *listen, uint32_t *arp)
+                                                    int32_t *listen, uint32_t *arp, unsigned long long *crow,
+                                                    CounterDelta d)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (crow != nullptr && i < (uint32_t)RXG_NCOUNTERS && d.v[i] != 0)  // (counters_add's work)
+        atomicAdd(crow + i, (unsigned long long)d.v[i]);
     if (i >= n) return;
     const MirrorPatch q = p[i];
     if (q.target == kPatchBucket)
@@ -230,10 +233,13 @@ __global__ __launch_bounds__(256) void mirror_patch(const MirrorPatch *p, uint32
 }
 
 hipError_t launch_mirror_patch(const MirrorPatch *p, uint32_t n, uint4 *buckets, int32_t *listen, uint32_t *arp,
-                               hipStream_t st)
+                               hipStream_t st, unsigned long long *crow, const CounterDelta *delta)
 {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(mirror_patch, dim3((n + 255u) / 256u), dim3(256), 0, st, p, n, buckets, listen, arp);
+    if (n == 0 && crow == nullptr) return hipSuccess;
+    CounterDelta d{};
+    if (crow != nullptr) d = *delta;
+    hipLaunchKernelGGL(mirror_patch, dim3(std::max(1u, (n + 255u) / 256u)), dim3(256), 0, st, p, n, buckets, listen,
+                       arp, crow, d);
     return hipGetLastError();
 }
 

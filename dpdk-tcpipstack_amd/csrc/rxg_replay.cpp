@@ -434,10 +434,9 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
     if (c->replay_cursor + 1 < c->last_bursts.size()) select_burst(c, c->replay_cursor + 1);
     bool nz = false;
     for (int k = 0; k < RXG_NCOUNTERS; ++k) nz |= delta[k] != 0;
-    if (nz) {  // add the corrections to the host row of the counter block, in stream order
-        CounterDelta d;
-        for (int k = 0; k < RXG_NCOUNTERS; ++k) d.v[k] = delta[k];
-        HIP_OK(launch_counters_add(c->counters + (size_t)(RXG_COUNTER_ROWS - 1) * RXG_NCOUNTERS, d, c->stream));
+    if (nz) {  // the corrections, added with the next mirror patch launch (flush_delta)
+        for (int k = 0; k < RXG_NCOUNTERS; ++k) c->pend_delta[k] += delta[k];
+        c->pend = true;
     }
     return 0;
 }

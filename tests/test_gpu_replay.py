@@ -18,6 +18,7 @@ import rxg
 
 pytestmark = pytest.mark.gpu
 LISTENING, SYN_RECV, ESTABLISHED, CLOSED = 1, 3, 4, 0
+COUNTER_ROWS = 65  # rxg.h RXG_COUNTER_ROWS: 64 kernel replicas + the replay's corrections
 
 
 class Model:
@@ -129,8 +130,9 @@ def test_replay_sequential_equivalence(replay_engine, seed):
     run_replay_equivalence(replay_engine, seed)
 
 
-def run_replay_equivalence(engine, seed, burst=None):
-    """burst(engine, frames) -> REC16 records: the burst form under test (default rxg_rx_burst)."""
+def run_replay_equivalence(engine, seed, burst=None, check_counters=None):
+    """burst(engine, frames) -> REC16 records: the burst form under test (default rxg_rx_burst).
+    check_counters(engine, expected, rows, frames): in place of the counters read."""
     rows, frames = scenario(seed)
     exp, ecnt, erows = sequential_reference(rows, frames)
     tcb, live = pktgen.table_arrays(rows)
@@ -168,7 +170,10 @@ def run_replay_equivalence(engine, seed, burst=None):
         elif v in (rxg.V_RST_NOPCB, rxg.V_RST_LISTEN_NONSYN):
             assert got[i] == ("rst",), (i, got[i], exp[i])
     assert model.rows == erows
-    assert engine.counters().tolist() == ecnt.tolist()
+    if check_counters:
+        check_counters(engine, ecnt, erows, frames)
+    else:
+        assert engine.counters().tolist() == ecnt.tolist()
     # the burst alone (snapshot semantics) would have differed: the scenario bites
     snap = [(int(r["verdict"]), int(r["tcb_idx"]), int(r["state"])) for r in recs]
     assert snap != exp
@@ -307,3 +312,31 @@ def test_arp_bucket_clusters_and_zero(engine):
         engine.arp_learned(ip)
     check(set(known) | set(clus[14:24]) | {0} | set(pool[:200]))
     engine.arp_disable()
+
+
+@pytest.mark.parametrize("path", ["dev_pointer", "reset", "next_burst"])
+def test_replay_corrections_reach_the_counter_block(replay_engine, path):
+    """The replay's counter corrections wait on the host for the context's next mirror patch
+    launch (csrc/rxg_replay.cpp, rxg_host.cpp flush_delta): read through rxg_counters_dev
+    after rxg_sync they are in the device block; a reset before the next burst zeroes them
+    with the rest; the next burst's patch launch carries them (its own counts added)."""
+    lib = rxg.load_library()
+
+    def check(engine, ecnt, rows, frames):
+        if path == "dev_pointer":
+            ptr = lib.rxg_counters_dev(engine.ctx)
+            block = np.zeros(COUNTER_ROWS * 16, dtype=np.uint64)
+            assert lib.rxg_memcpy_d2h(engine.ctx, block.ctypes.data, ptr, block.nbytes, None) == 0
+            engine.sync()
+            assert block.reshape(COUNTER_ROWS, 16).sum(axis=0).tolist() == ecnt.tolist()
+        elif path == "reset":
+            engine.counters_reset()
+            assert engine.counters().tolist() == [0] * 16
+        else:
+            arena, off, lens = pktgen.pack_arena(frames)
+            tcb, live = pktgen.table_arrays(rows)
+            _, c2 = oracle.rx_batch(arena, off, lens, tcb, live)  # the next burst, against the new table
+            engine.rx_burst(frames, rxg.REC16)
+            assert engine.counters().tolist() == (ecnt + c2).tolist()
+
+    run_replay_equivalence(replay_engine, 4, check_counters=check)
