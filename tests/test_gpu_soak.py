@@ -135,3 +135,63 @@ def test_soak_served_bursts():
         eng.close()
     print(f"served soak: {cases} batches bit-exact")
     assert cases > 0
+
+
+@pytest.mark.skipif(BUDGET <= 0, reason="opt-in soak: set RXG_SOAK=<seconds>")
+def test_soak_fused_hand_off():
+    """The burst with its payload hand-off in one pass (rxg_rx_burst_payload_dev, DESIGN.md
+    §5.F) over random parity batches and grids: the copy form (payload lines into a sentinel
+    arena) and the by-reference form (messages staged in the record ring, flushing mid-stream
+    on small grids), every record kind -- records, counters, messages and payload bytes
+    bit-exact with the oracle, and no line outside a payload written."""
+    from oracle import payload as opl
+    t_end = time.time() + BUDGET
+    master = random.Random(int(os.environ.get("RXG_SOAK_SEED", "2028")))
+    engines, cases, t_print = {}, 0, time.time()
+    try:
+        while time.time() < t_end:
+            seed = master.randrange(1 << 30)
+            rng = random.Random(seed)
+            n = rng.choice([1, 31, 64, 65, 200, 1000, 4096, 9000])
+            rows, frames = pktgen.parity_set(seed=seed, n=n, nflows=rng.choice([3, 50, 400]))
+            for _ in range(rng.randrange(0, 4)):  # runs of small frames of a few flows
+                a = rng.randrange(0, n)
+                for i in range(a, min(n, a + rng.randrange(64, 700))):
+                    frames[i] = pktgen.frame(src_ip=0x0A000001 + (i % 3), sport=1024 + (i % 3), dport=80,
+                                             payload=bytes(rng.randrange(0, 11)))
+            kind = rng.choice([rxg.REC8, rxg.REC16, rxg.REC48])
+            blocks = rng.choice([0, 1, 2, 3, 5, 13, 40])  # 0: the product grid
+            by_ref = rng.random() < 0.5
+            if blocks not in engines:
+                engines[blocks] = rxg.Engine(device=0, max_batch=1 << 14, max_bytes=32 << 20, max_blocks=blocks)
+            eng = engines[blocks]
+            tcb, live = pktgen.table_arrays(rows)
+            eng.tcb_load(tcb, live)
+            eng.counters_reset()
+            recs, pay, msgs, (arena, off, lens) = eng.rx_burst_payload(frames, kind, arena_fill=0xA5,
+                                                                       by_reference=by_ref)
+            exp, ecnt = oracle.rx_batch(arena, off, lens, tcb, live)
+            want = exp if kind == rxg.REC48 else exp["c"] if kind == rxg.REC16 else rxg.rec8_pack(exp["c"])
+            what = f"seed {seed} n {n} kind {kind} blocks {blocks} by_ref {by_ref}"
+            assert recs.tobytes() == want.tobytes(), what + ": records differ"
+            assert eng.counters().tolist() == ecnt.tolist(), what + ": counters differ"
+            e_msgs, pays = opl.slots(frames, exp["c"], off)
+            for name in ("arena_off", "len", "flags"):
+                assert np.array_equal(msgs[name], e_msgs[name]), what + f": msgs.{name} differ"
+            mask = np.zeros(len(pay), dtype=bool)
+            for i, p in enumerate(pays):
+                if p is not None:
+                    o = int(msgs[i]["arena_off"])
+                    assert pay[o:o + len(p)].tobytes() == p, what + f": frame {i} payload differs"
+                    mask[o // 64 * 64:(o + len(p) + 63) // 64 * 64] = True
+            if not by_ref:
+                assert (pay[~mask] == 0xA5).all(), what + ": a line holding no payload was written"
+            cases += 1
+            if time.time() - t_print > 20:
+                print(f"fused soak: {cases} batches", flush=True)
+                t_print = time.time()
+    finally:
+        for e in engines.values():
+            e.close()
+    print(f"fused soak: {cases} batches bit-exact")
+    assert cases > 0
