@@ -39,6 +39,16 @@ def test_library_exports_every_declared_symbol():
     assert set(declared_functions()) <= exported
 
 
+def test_library_exports_only_the_c_abi():
+    """A linker version script (csrc/rxg.map) keeps the C++ internals -- the context helpers
+    of csrc/rxg_ctx.h, the rxg:: host functions, the standard-library instantiations -- out
+    of the dynamic symbol table: every defined export is an rxg_* entry point."""
+    out = subprocess.run(["nm", "-D", "--defined-only", rxg.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    names = [line.split()[-1] for line in out.splitlines() if line.strip()]
+    assert names and all(n.startswith("rxg_") for n in names), [n for n in names if not n.startswith("rxg_")][:10]
+
+
 def test_library_has_gfx950_code_object():
     data = open(rxg.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data
