@@ -97,6 +97,8 @@ struct rxg_ctx {
     // (C4 on a caller stream 78.2 -> 73.2 us per launch, C2 24.5 -> 20.3).
     hipEvent_t mirror_ev = nullptr;
     bool mirror_ev_set = false;
+    bool mirror_ev_stale = false;  // a write on `stream` after mirror_ev's last recording
+                                   // (recorded when another stream or the server needs it)
     uint64_t table_writes = 0;  // mirror_ev recordings (device table writes) so far
     struct Reader {
         hipStream_t s;
@@ -118,6 +120,15 @@ struct rxg_ctx {
         bool set = false;
     } patch[kPatchBufs];
     int patch_next = 0;
+    // With a large BAR the patch buffers are device memory the host writes through the BAR,
+    // and a launch on `stream` carries the burst's patch list itself (launch_bursts: no patch
+    // launch before it); defer_patch asks apply_patches for that, ip_* is the list taken.
+    bool patch_dev = false;
+    bool launch_patches = true;  // (experiment build: RXG_LAUNCH_PATCHES=0 turns the carrying off)
+    bool defer_patch = false;
+    const rxg::MirrorPatch *ip_list = nullptr;
+    uint32_t ip_n = 0;
+    int ip_buf = -1;
 
     unsigned long long *counters = nullptr;
     // the replays' counter corrections not yet on the device: added by the next mirror patch
@@ -236,6 +247,10 @@ struct rxg_ctx {
     } srv;
 };
 
+// patch lists longer than this go through their own launch (every workgroup of a launch that
+// carries a list stores all of it)
+inline constexpr uint32_t kLaunchPatchMax = 256;
+
 inline constexpr size_t kCounterBytes = (size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS * sizeof(uint64_t);
 
 struct rxg_event {
@@ -279,6 +294,8 @@ void select_burst(rxg_ctx *c, uint32_t j);
 int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
                  const char *who, uint32_t stride64 = 0);
 int burst_offsets(rxg_ctx *c, hipStream_t st, const uint32_t **out);
+// mirror_ev recorded on `stream` if a write since its last recording has not been (rxg_host.cpp)
+int mirror_event(rxg_ctx *c);
 // the pending counter corrections (rxg_ctx::pend_delta) to the device, on c->stream
 int flush_delta(rxg_ctx *c);
 

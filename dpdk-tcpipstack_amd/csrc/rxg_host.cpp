@@ -77,6 +77,11 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
         // against 177)
         c->grid_pay = cus * 2u;
     }
+    // a large BAR: the mirror's patch lists live in device memory the host writes directly,
+    // and a burst launch carries its own (launch_bursts)
+    int large_bar = 0;
+    c->patch_dev = hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) == hipSuccess &&
+                   large_bar != 0;
     if (cfg) {
         c->replay_on_device = (cfg->flags & RXG_CFG_REPLAY_ON_DEVICE) != 0;
         c->lazy_readers = (cfg->flags & RXG_CFG_STREAMS_OUTLIVE_WRITES) != 0;
@@ -91,6 +96,7 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     if (const char *v = getenv("RXG_ZC_BYTES")) c->zc_bytes = strtoull(v, nullptr, 10);
     if (const char *v = getenv("RXG_MIRROR_REBUILD")) c->mirror_rebuild = atoi(v);
     if (const char *v = getenv("RXG_REPLAY_COARSE")) c->replay_coarse = atoi(v);
+    if (const char *v = getenv("RXG_LAUNCH_PATCHES")) c->launch_patches = atoi(v) != 0;
     if (const char *v = getenv("RXG_MIRROR_LOAD_PCT")) c->mir.max_load_pct = (uint32_t)atoi(v);
     if (c->replay_coarse) c->replay_on_device = true;
 #endif
@@ -160,7 +166,7 @@ extern "C" int rxg_fini(rxg_ctx *c)
     if (c->h_pm) (void)hipHostFree(c->h_pm);
     if (c->pm_ev) (void)hipEventDestroy(c->pm_ev);
     for (auto &pb : c->patch) {
-        if (pb.h) (void)hipHostFree(pb.h);
+        if (pb.h) (void)(c->patch_dev ? hipFree(pb.h) : hipHostFree(pb.h));
         if (pb.ev) (void)hipEventDestroy(pb.ev);
     }
     for (auto &r : c->readers) (void)hipEventDestroy(r.e);
@@ -366,32 +372,17 @@ static int sync_table_readers(rxg_ctx *c)
     return 0;
 }
 
-// A mirror's patches (at most one per device word), in one launch on c->stream.
-template <typename M>
-static int apply_patches(rxg_ctx *c, M &mirror)
+// A patch list in c->patch[bi] (n patches) as its own launch on c->stream.
+static int launch_patch_list(rxg_ctx *c, int bi, uint32_t n)
 {
-    const std::vector<MirrorPatch> &p = mirror.patches;
-    if (p.empty()) return 0;
-    rxg_ctx::PatchBuf &pb = c->patch[c->patch_next];
-    c->patch_next = (c->patch_next + 1) % rxg_ctx::kPatchBufs;
-    if (pb.set) HIP_OK(hipEventSynchronize(pb.ev));  // this buffer's kernel has read it
-    pb.set = false;
-    if (p.size() > pb.cap) {
-        if (pb.h) HIP_OK(hipHostFree(pb.h));
-        pb.h = nullptr;
-        pb.cap = 0;
-        const uint32_t cap = (uint32_t)std::max<size_t>(p.size() * 2, 1024);
-        HIP_OK(hipHostMalloc((void **)&pb.h, (size_t)cap * sizeof(MirrorPatch), hipHostMallocDefault));
-        pb.cap = cap;
-    }
-    std::memcpy(pb.h, p.data(), p.size() * sizeof(MirrorPatch));
+    rxg_ctx::PatchBuf &pb = c->patch[bi];
     int rc = wait_table_readers(c);
     if (rc) return rc;
     // the last replay's counter corrections ride along (its table writes are why this runs)
     CounterDelta d;
     if (c->pend) std::memcpy(d.v, c->pend_delta, sizeof d.v);
-    HIP_OK(launch_mirror_patch(pb.h, (uint32_t)p.size(), (uint4 *)c->buckets.p, (int32_t *)c->listen.p,
-                               (uint32_t *)c->d_arp.p, c->stream, c->pend ? correction_row(c) : nullptr, &d));
+    HIP_OK(launch_mirror_patch(pb.h, n, (uint4 *)c->buckets.p, (int32_t *)c->listen.p, (uint32_t *)c->d_arp.p,
+                               c->stream, c->pend ? correction_row(c) : nullptr, &d));
     if (c->pend) {
         std::memset(c->pend_delta, 0, sizeof c->pend_delta);
         c->pend = false;
@@ -400,8 +391,67 @@ static int apply_patches(rxg_ctx *c, M &mirror)
     pb.set = true;
     HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
     c->mirror_ev_set = true;
-    ++c->table_writes;
+    c->mirror_ev_stale = false;
+    return 0;
+}
+
+// A mirror's patches (at most one per device word): into the next patch buffer, then in one
+// launch on c->stream -- or, when the caller is about to launch a burst on c->stream that
+// can carry them (c->defer_patch, launch_bursts), left for that launch (c->ip_*).
+template <typename M>
+static int apply_patches(rxg_ctx *c, M &mirror)
+{
+    const std::vector<MirrorPatch> &p = mirror.patches;
+    if (p.empty()) return 0;
+    const uint32_t n = (uint32_t)p.size();
+    const int bi = c->patch_next;
+    rxg_ctx::PatchBuf &pb = c->patch[bi];
+    c->patch_next = (bi + 1) % rxg_ctx::kPatchBufs;
+    if (pb.set) HIP_OK(hipEventSynchronize(pb.ev));  // the launch that read this buffer is done
+    pb.set = false;
+    if (n > pb.cap) {
+        if (pb.h) HIP_OK(c->patch_dev ? hipFree(pb.h) : hipHostFree(pb.h));
+        pb.h = nullptr;
+        pb.cap = 0;
+        const uint32_t cap = std::max<uint32_t>(n * 2u, 1024u);
+        const size_t bytes = (size_t)cap * sizeof(MirrorPatch);
+        if (c->patch_dev)
+            HIP_OK(hipExtMallocWithFlags((void **)&pb.h, bytes, hipDeviceMallocFinegrained));
+        else
+            HIP_OK(hipHostMalloc((void **)&pb.h, bytes, hipHostMallocDefault));
+        pb.cap = cap;
+    }
+    std::memcpy(pb.h, p.data(), (size_t)n * sizeof(MirrorPatch));
+    if (c->patch_dev) _mm_sfence();  // write-combined through the BAR: out before the launch
     mirror.patches_taken();
+    ++c->table_writes;
+    if (c->defer_patch && c->ip_n == 0 && n <= kLaunchPatchMax) {
+        c->ip_list = pb.h;
+        c->ip_n = n;
+        c->ip_buf = bi;
+        c->mirror_ev_set = true;
+        c->mirror_ev_stale = true;  // the carrying launch is the write (mirror_event)
+        return 0;
+    }
+    return launch_patch_list(c, bi, n);
+}
+
+// A carried list the burst did not take (a failure between the sync and the launch): as its
+// own launch, so no write is lost.
+static int launch_carried_patches(rxg_ctx *c)
+{
+    if (c->ip_n == 0) return 0;
+    const uint32_t n = c->ip_n;
+    c->ip_n = 0;
+    return launch_patch_list(c, c->ip_buf, n);
+}
+
+int mirror_event(rxg_ctx *c)
+{
+    if (c->ip_n) return launch_carried_patches(c);  // (not between a sync and its burst)
+    if (!c->mirror_ev_stale) return 0;
+    HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
+    c->mirror_ev_stale = false;
     return 0;
 }
 
@@ -431,6 +481,7 @@ int tcb_push(rxg_ctx *c)
         HIP_OK(hipStreamSynchronize(c->stream));
         HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
         c->mirror_ev_set = true;
+        c->mirror_ev_stale = c->ip_n != 0;  // (a list a burst is to carry comes after it)
         ++c->table_writes;
     } else if ((rc = apply_patches(c, m))) {
         return rc;
@@ -492,6 +543,7 @@ static int arp_sync(rxg_ctx *c)
         HIP_OK(hipStreamSynchronize(c->stream));
         HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
         c->mirror_ev_set = true;
+        c->mirror_ev_stale = c->ip_n != 0;  // (a list a burst is to carry comes after it)
         ++c->table_writes;
     } else if ((rc = apply_patches(c, a))) {
         return rc;
@@ -521,6 +573,7 @@ static int order_table_reader_before(rxg_ctx *c, hipStream_t st)
     // is a barrier packet between the caller's launches)
     for (auto &x : c->readers)
         if (x.s == st && x.waited == c->table_writes) return 0;
+    if (int rc = mirror_event(c)) return rc;  // (a write a burst carried: recorded now)
     HIP_OK(hipStreamWaitEvent(st, c->mirror_ev, 0));
     for (auto &x : c->readers)
         if (x.s == st) x.waited = c->table_writes;
@@ -692,8 +745,22 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
     if (c->lazy_readers && st != c->stream && !stream_registered(c, st))
         return fail(-EINVAL, "%s: table-reading launch on stream %p, not registered with rxg_stream_register "
                              "(RXG_CFG_STREAMS_OUTLIVE_WRITES)", who, (void *)st);
+    // The burst's first launch carries the mirror's patch list when nothing else reads the
+    // tables meanwhile: launched on the context's stream (ordered after every earlier reader
+    // there), no reader pending on another stream, and frames in that launch (a launch of
+    // none is never made).  It then replaces a patch launch: ≈ 10 µs of host launch latency
+    // per churning burst.
+    bool first_has_frames = false;
+    for (uint32_t j = 0; j < std::min(k, kMaxBursts); ++j) first_has_frames |= bursts[j].n != 0;
+    bool others_pending = false;
+    for (const auto &r : c->readers) others_pending |= r.pending;
+    c->defer_patch = c->launch_patches && c->patch_dev && st == c->stream && first_has_frames && !others_pending;
     int rc = begin_bursts(c, frames, bursts, k, rec_kind, who, stride64);
-    if (rc) return rc;
+    c->defer_patch = false;
+    if (rc) {
+        (void)launch_carried_patches(c);
+        return rc;
+    }
     if ((rc = order_table_reader_before(c, st))) return rc;
     LaunchBurst lb[kMaxBursts];
     for (uint32_t j0 = 0; j0 < k; j0 += kMaxBursts) {
@@ -719,7 +786,21 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
                      : pay ? (rec_kind == RXG_REC48 ? c->grid_ref48 : rec_kind == RXG_REC8 ? c->grid_ref8 : c->grid_ref16)
                      : (rec_kind == RXG_REC48 ? c->grid_rec48 : rec_kind == RXG_REC8 ? c->grid_rec8 : c->grid_rec16);
         if (L.max_blocks == 0) L.max_blocks = 1024;
-        HIP_OK(rx_launch(c, L, st));
+        const bool carries = j0 == 0 && c->ip_n != 0;
+        if (carries) {
+            L.ipatch = c->ip_list;
+            L.nipatch = c->ip_n;
+        }
+        const hipError_t e = rx_launch(c, L, st);
+        if (e != hipSuccess) {
+            (void)launch_carried_patches(c);
+            HIP_OK(e);
+        }
+        if (carries) {  // the list's buffer is free again once this launch has run
+            c->ip_n = 0;
+            HIP_OK(hipEventRecord(c->patch[c->ip_buf].ev, st));
+            c->patch[c->ip_buf].set = true;
+        }
     }
     if ((rc = order_table_reader_after(c, st))) return rc;
     c->burst_ok = true;

@@ -8,6 +8,8 @@
 
 namespace rxg {
 
+struct MirrorPatch;  // rxg_mirror.h
+
 // One launch classifies up to kMaxBursts bursts whose frames share one pool (`frames`):
 // burst k's frame i is at frames + 64 * off64[i], its record at out + i * record size.
 constexpr uint32_t kMaxBursts = 32;
@@ -32,6 +34,10 @@ struct LaunchRx {
     uint8_t *pay_arena;    // non-null (with pay_msgs): the payload hand-off fused in (one burst,
     rxg_payload_msg *pay_msgs;  //   record kind 8 / 16 / 48; rxg_rx_burst_payload_dev)
     int variant;           // experiment library only (launch_rx_exp): RXG_VARIANT
+    // mirror patches the launch applies before its first probe, in place of a patch launch
+    // before it (rxg_host.cpp launch_bursts; the list in device memory, kInlinePatchMax at most)
+    const MirrorPatch *ipatch;
+    uint32_t nipatch;
 };
 
 struct LaunchSynth {
@@ -166,7 +172,6 @@ hipError_t launch_synth(const LaunchSynth &L, hipStream_t st);
 // off[i] = slot0 + i * stride64, i < n (a fixed-stride burst's offsets as a list)
 hipError_t launch_strided_offsets(uint32_t *off, uint32_t n, uint32_t slot0, uint32_t stride64, hipStream_t st);
 // rxg_mirror.h patches (n of them, host-visible memory) applied to the device mirror tables
-struct MirrorPatch;
 // Replay counter corrections (two's complement: a negative delta wraps the uint64 sum)
 struct CounterDelta {
     int64_t v[RXG_NCOUNTERS];

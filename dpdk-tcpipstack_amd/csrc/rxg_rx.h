@@ -378,6 +378,9 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     const int wid = threadIdx.x >> 6;
     const uint32_t wave = blk * 4u + (uint32_t)wid;
     const uint32_t nwaves = nblk * 4u;
+    if constexpr (!SRV) {
+        if (a.nipatch != 0u) apply_launch_patches(a);  // (kernel argument: uniform)
+    }
 
     WaveCounters wc;
 #pragma unroll
@@ -623,6 +626,8 @@ inline hipError_t rx_args(const LaunchRx &L, RxArgs &a, RxGrid &g)
     a.stride64 = L.stride64;
     a.pay_arena = L.pay_arena;
     a.pay_msgs = L.pay_msgs;
+    a.ipatch = L.ipatch;
+    a.nipatch = L.nipatch;
     if (L.nbursts > kMaxBursts) return hipErrorInvalidValue;
     uint32_t nslices = 0;
     for (uint32_t k = 0; k < L.nbursts; ++k) {

@@ -98,6 +98,9 @@ struct RxArgs {
     // other fields keep their offsets.)
     uint8_t *pay_arena;
     rxg_payload_msg *pay_msgs;
+    // mirror patches to store before the first probe (LaunchRx::ipatch; never the server's)
+    const MirrorPatch *ipatch;
+    uint32_t nipatch;
 };
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -197,6 +200,28 @@ __device__ __forceinline__ uint32_t slice_frames(const RxArgs &a, uint32_t s, BC
 struct Rec {
     uint4 q0, q1, q2;
 };
+
+// The mirror patches a launch carries (LaunchRx::ipatch, in place of a mirror_patch launch
+// before it): every workgroup stores all of them before its first table read -- the same
+// values to the same words, so none needs another's (no grid-wide order), and each waits
+// for its own stores before its waves read the tables.  Few (kInlinePatchMax), by contract.
+__device__ __forceinline__ void apply_launch_patches(const RxArgs &a)
+{
+    uint4 *buckets = const_cast<uint4 *>(a.t.buckets);
+    int32_t *listen = const_cast<int32_t *>(a.t.listen);
+    uint32_t *arp = reinterpret_cast<uint32_t *>(const_cast<uint4 *>(a.t.arp));
+    for (uint32_t i = threadIdx.x; i < a.nipatch; i += blockDim.x) {
+        const MirrorPatch q = a.ipatch[i];
+        if (q.target == kPatchBucket)
+            buckets[q.index] = make_uint4(q.v[0], q.v[1], q.v[2], q.v[3]);
+        else if (q.target == kPatchListen)
+            listen[q.index] = (int32_t)q.v[0];
+        else
+            arp[q.index] = q.v[0];
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the stores acknowledged (vmcnt counts stores on gfx9)
+    __syncthreads();
+}
 
 // ------------------------------------------------- fused payload hand-off (PAY) ---
 // The PAY template argument: no hand-off, the hand-off with its payload lines copied to the

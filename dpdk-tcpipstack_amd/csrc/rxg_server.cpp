@@ -258,6 +258,7 @@ static int server_burst(rxg_ctx *c, const rxg_dev_batch *b, bool inl, bool large
     if (rc) return rc;
     // mirror writes queued on the context's stream land before the server reads the tables
     if (c->table_writes != c->srv.synced_writes) {
+        if ((rc = mirror_event(c))) return rc;  // (a write a burst carried: recorded now)
         HIP_OK(hipEventSynchronize(c->mirror_ev));
         c->srv.synced_writes = c->table_writes;
     }

@@ -486,8 +486,8 @@ int rxg_counters_read(rxg_ctx *ctx, uint64_t *out);
 /* Device address of the uint64[RXG_COUNTER_ROWS][RXG_NCOUNTERS] block: an in-place RCCL
    all-reduce (sum) over it followed by rxg_counters_read merges counters across GPUs.  The
    replay's corrections reach the block in the context's stream order: with the next mirror
-   update a burst launches, or at the latest at rxg_counters_read, rxg_sync or this call
-   (read the block after the context's stream, as for the kernels' own counts). */
+   patch launch, or at the latest at rxg_counters_read, rxg_sync or this call (read the
+   block after the context's stream, as for the kernels' own counts). */
 void *rxg_counters_dev(rxg_ctx *ctx);
 
 /* ------------------------------------------------------------------------- */
