@@ -80,8 +80,13 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
     // a large BAR: the mirror's patch lists live in device memory the host writes directly,
     // and a burst launch carries its own (launch_bursts)
     int large_bar = 0;
-    c->patch_dev = hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) == hipSuccess &&
-                   large_bar != 0;
+    if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) == hipSuccess && large_bar) {
+        void *probe = nullptr;  // and host-writable device memory can be had
+        if (hipExtMallocWithFlags(&probe, 4096, hipDeviceMallocFinegrained) == hipSuccess) {
+            (void)hipFree(probe);
+            c->patch_dev = true;
+        }
+    }
     if (cfg) {
         c->replay_on_device = (cfg->flags & RXG_CFG_REPLAY_ON_DEVICE) != 0;
         c->lazy_readers = (cfg->flags & RXG_CFG_STREAMS_OUTLIVE_WRITES) != 0;
