@@ -164,6 +164,14 @@ static void tcp_record_counters(const rxg_rec16 &r, int64_t sign, int64_t *d)
 
 // The pass-1 key of a frame of >= 54 bytes, as the kernel forms it: ports = dport << 16 |
 // sport (host order), ipv4_dst as loaded, ipv4_src host order (tcp_tcb.c:134-135,152-155).
+// The replay's written-tuple filter index (16 bits): every packet after a burst's first table
+// write is checked against it, so two multiplies rather than the table's seven (tuple_hash;
+// 14 -> 6 ns a packet on this container's core); a collision only costs the exact lookup.
+static inline uint32_t filter_hash(const TupleKey &k)
+{
+    return (k.ports * 0x9E3779B1u + k.src * 0x85EBCA6Bu + k.dst) >> 16;
+}
+
 static inline TupleKey frame_key(const uint8_t *f)
 {
     const uint32_t sport = ((uint32_t)f[34] << 8) | f[35], dport = ((uint32_t)f[36] << 8) | f[37];
@@ -279,7 +287,7 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         if (pass2) minnull_seq = bulk_seq = wseq;
         for (const TupleKey &k : keys) {
             key_seq[k] = wseq;
-            const uint32_t h = tuple_hash(k.ports, k.dst, k.src);
+            const uint32_t h = filter_hash(k);
             if (!filt_used) {
                 filt.assign(1024, 0ull);
                 filt_used = true;
@@ -318,7 +326,7 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
         if (all_seq > s || (q.flags & RXG_F_TRUNC)) return true;
         const TupleKey k = frame_key((const uint8_t *)frames[j]);
         if (filt_used) {
-            const uint32_t h = tuple_hash(k.ports, k.dst, k.src);
+            const uint32_t h = filter_hash(k);
             if ((filt[(h >> 6) & 1023u] >> (h & 63u)) & 1ull) {
                 auto it = key_seq.find(k);
                 if (it != key_seq.end() && it->second > s) return true;
