@@ -108,10 +108,11 @@ struct rxg_ctx {
         uint64_t waited;  // table_writes when `s` last waited for mirror_ev (~0: never)
     };
     std::vector<Reader> readers;
-    // Patch upload ring: the patch kernel reads its list from pinned host memory over PCIe,
-    // so a buffer is reused only after its kernel ran; kPatchBufs buffers, each with its
-    // event, and the host waits only when all of them are in flight (a patch kernel waits on
-    // the device for bursts running on caller streams, which can be long).
+    // Patch upload ring: a list is read by its patch kernel or by the burst that carries it
+    // (device memory the host writes through a large BAR, else pinned host memory read over
+    // PCIe), so a buffer is reused only after that launch ran; kPatchBufs buffers, each with
+    // its event, and the host waits only when all of them are in flight (a patch kernel waits
+    // on the device for bursts running on caller streams, which can be long).
     static constexpr int kPatchBufs = 4;
     struct PatchBuf {
         rxg::MirrorPatch *h = nullptr;
