@@ -301,3 +301,42 @@ def test_rejected_launch_keeps_the_previous_burst_replayable():
             if isinstance(v, rxg.DevArray):
                 v.free()
         engine.close()
+
+
+def test_carried_patches_then_a_burst_on_another_stream(engine):
+    """A few writes (a list the next burst on the context's stream carries itself, DESIGN.md
+    §2.1), that burst, then at once a burst on a caller stream: the second must see the new
+    table, though no patch launch ran -- it waits for the event recorded after the carrying
+    burst when it is needed (mirror_event) -- and so must a third on the context's stream."""
+    n, nflows = 1 << 16, 1000
+    dev = engine.synth(n=n, nflows=nflows, len_a=576, seed=91, with_flows=True)
+    t0, l0 = rxg.synthetic_tcb_table(nflows)
+    flows = dev["flow"].download(np.uint32, n)
+    outs = [engine.alloc(n * 16) for _ in range(3)]
+    s2 = torch.cuda.Stream()
+    try:
+        for rnd in range(3):
+            engine.tcb_load(t0, l0)
+            engine.tcb_sync()
+            engine.sync()
+            torch.cuda.synchronize()
+            removed = set(range(1 + rnd, nflows + 1, 97))  # ~10 removals: a carried list
+            for i in sorted(removed):
+                engine.tcb_remove(i)
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, outs[0].ptr, 16, None)
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, outs[1].ptr, 16,
+                                s2.cuda_stream)
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, outs[2].ptr, 16, None)
+            torch.cuda.synchronize()
+            engine.sync()
+            gone = np.isin(flows.astype(np.int64) + 1, sorted(removed))
+            for o in outs:
+                r = o.download(rxg.REC16_DTYPE, n)
+                assert (r["tcb_idx"][~gone] == flows[~gone].astype(np.int32) + 1).all()
+                assert (r["tcb_idx"][gone] == 0).all() and (r["verdict"][gone] == rxg.V_RST_LISTEN_NONSYN).all()
+    finally:
+        for d in outs:
+            d.free()
+        for v in dev.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()
