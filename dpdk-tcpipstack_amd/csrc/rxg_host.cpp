@@ -409,6 +409,19 @@ static int apply_patches(rxg_ctx *c, M &mirror)
     const std::vector<MirrorPatch> &p = mirror.patches;
     if (p.empty()) return 0;
     const uint32_t n = (uint32_t)p.size();
+    if (c->defer_patch && c->ip_n != 0) {
+        // a second table's patches (the ARP mirror's after the TCB mirror's) join the list
+        // the burst carries, when it has room (the kernel applies each by its target)
+        rxg_ctx::PatchBuf &cb = c->patch[c->ip_buf];
+        if (c->ip_n + n <= kLaunchPatchMax && c->ip_n + n <= cb.cap) {
+            std::memcpy(cb.h + c->ip_n, p.data(), (size_t)n * sizeof(MirrorPatch));
+            if (c->patch_dev) _mm_sfence();
+            mirror.patches_taken();
+            ++c->table_writes;
+            c->ip_n += n;
+            return 0;
+        }
+    }
     const int bi = c->patch_next;
     rxg_ctx::PatchBuf &pb = c->patch[bi];
     c->patch_next = (bi + 1) % rxg_ctx::kPatchBufs;

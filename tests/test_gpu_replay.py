@@ -229,6 +229,15 @@ def test_arp_learn_flag_and_replay(engine):
     assert lib.rxg_rx_replay(engine.ctx, C.byref(ops), ptrs, ptrs, recs.ctypes.data, len(bufs), 16) == 0
     assert calls == exp
     assert engine.arp_count() == len(known) + len(exp)
+    # a TCB write beside the learned addresses: the next burst takes both mirrors' patches
+    # (one list the burst itself carries on a large-BAR box)
+    dst_raw = pktgen.raw_of_host(pktgen.ip4(192, 168, 78, 2))
+    engine.tcb_upsert(1, 80, 5555, dst_raw, unknown[0], 4)
+    probe = [pktgen.frame(src_ip=unknown[0], sport=5555, flags=0x10)] + frames
+    recs_b = engine.rx_burst(probe, rxg.REC16)
+    assert int(recs_b[0]["verdict"]) == rxg.V_DISPATCH and int(recs_b[0]["tcb_idx"]) == 1
+    assert not (recs_b["flags"] & rxg.F_ARP_LEARN).any()
+    engine.tcb_remove(1)
     # a second burst of the same frames learns nothing new
     recs2 = engine.rx_burst(frames, rxg.REC16)
     assert not (recs2["flags"] & rxg.F_ARP_LEARN).any()
