@@ -61,6 +61,21 @@ def traffic_of(name, n, rec):
         with open(os.path.join(ROOT, tf)) as fh:
             return json.load(fh)["hbm_bytes_per_launch"], tf
     return None, None
+
+
+def traffic_provenance(tf, lib_build: str) -> dict:
+    """Whether a traffic file counts the library this process runs: the src= hash its counted
+    runs loaded (stamped by scripts/pmc_traffic.py --prov; None for an unstamped file, as every
+    file before round 6) against the src= hash of lib_build (rxg_build_info)."""
+    stamped = None
+    if tf and os.path.exists(os.path.join(ROOT, tf)):
+        with open(os.path.join(ROOT, tf)) as fh:
+            stamped = json.load(fh).get("source_hash")
+    built = next((w[4:] for w in (lib_build or "").split() if w.startswith("src=")), None)
+    return {"traffic_src": stamped, "build_src": built,
+            "traffic_matches_build": stamped is not None and stamped == built}
+
+
 WORKLOADS = {
     # name: (frame_len, flows, mix, rotating copies)
     "c3_1500B_1Kflows": (1500, 1000, 0, 2),  # 2 rotating 1.5 GiB batches: no step re-reads the last one's tail from the 256 MB MALL
@@ -939,6 +954,8 @@ def main():
     barrier(device)
 
     traffic, traffic_src = traffic_of(args.workload, wl.n, args.rec)
+    prov = rxg.build_provenance()
+    tprov = traffic_provenance(traffic_src, prov["build"])
 
     if rank == 0:
         line = {
@@ -972,6 +989,9 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src,
+                         # the traffic file's counted build against the library measured here
+                         "traffic_src": tprov["traffic_src"],
+                         "traffic_matches_build": tprov["traffic_matches_build"],
                          "kernel_us": round(k_max_s * 1e6, 2),
                          "kernel_us_per_launch_pairs_rank0_median": round(k_med_s * 1e6, 2),
                          "kernel_us_min_over_ranks": round(k_min_s * 1e6, 2),
@@ -985,7 +1005,7 @@ def main():
             "counters_ok": bool(checks_ok),
             "counters": C,
             "legs": legs,
-            **rxg.build_provenance(),  # build (src= hash, rev=), lib, source_hash, build_matches_tree
+            **prov,  # build (src= hash, rev=), lib, source_hash, build_matches_tree
             "pg_timeout_s": args.pg_timeout if dist.is_initialized() else None,
         }
         print(json.dumps(line), flush=True)

@@ -7,13 +7,7 @@
 #include "rxg.h"
 #include "buildid.h"
 
-#ifdef RXG_EXPERIMENTS
-#define RXG_BUILD_KIND " experiments"
-#else
-#define RXG_BUILD_KIND ""
-#endif
-
 extern "C" const char *rxg_build_info(void)
 {
-    return "rxg src=" RXG_SRC_HASH " rev=" RXG_GIT_REV " built=" __DATE__ " " __TIME__ " gfx950" RXG_BUILD_KIND;
+    return "rxg src=" RXG_SRC_HASH " rev=" RXG_GIT_REV " built=" __DATE__ " " __TIME__ " gfx950";
 }

@@ -26,10 +26,7 @@ namespace rxg {
 //   min_null: lowest removed slot index (pass 2 would dereference NULL there).
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-#ifndef RXG_SLOTS_PER_BUCKET
-#define RXG_SLOTS_PER_BUCKET 4
-#endif
-constexpr int kSlotsPerBucket = RXG_SLOTS_PER_BUCKET;
+constexpr int kSlotsPerBucket = 4;
 constexpr uint32_t kIdxMask = 0x00FFFFFFu;
 constexpr int kStateShift = 24;
 constexpr int32_t kMaxTcbs = 0x00FFFFFF;  // indices 0 .. kMaxTcbs-1
@@ -39,14 +36,6 @@ RXG_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
 RXG_HD uint32_t tuple_hash(uint32_t ports, uint32_t dst_raw, uint32_t src_host)
 {
-#ifdef RXG_HASH_LITE
-    // experiment build (make exp-hash): two multiplies instead of seven; the same bucket
-    // occupancy on the synthetic flow sets (full buckets 1.95 % against 1.86 % at 64 K flows)
-    uint32_t g = (src_host ^ 0x9E3779B9u) * 0x85EBCA6Bu;
-    g ^= ports ^ rotl32(dst_raw, 16);
-    g *= 0xC2B2AE35u;
-    return g ^ (g >> 15);
-#endif
     uint32_t h = 0x9E3779B9u ^ (ports * 0xCC9E2D51u);
     h = rotl32(h, 13) * 5u + 0xE6546B64u;
     h ^= rotl32(dst_raw * 0xCC9E2D51u, 15) * 0x1B873593u;

@@ -64,16 +64,7 @@ struct rxg_ctx {
     uint32_t grid_pay = 512;        // rxg_rx_burst_payload_dev's grid (set at init)
     uint32_t grid_rec8 = 0, grid_rec16 = 0, grid_rec48 = 0, grid_tx = 0;
     uint32_t grid_ref8 = 0, grid_ref16 = 0, grid_ref48 = 0;  // the by-reference hand-off's
-    // Experiment switches: only an experiment build (make experiments, -DRXG_EXPERIMENTS,
-    // rxg/librxg_exp.so for scripts/kbench.py and pgbench.py) reads them from the
-    // environment; in the product library they stay 0.
     rxg::PackPool pack_pool;  // rxg_rx_burst's packing threads
-    int variant = 0;     // RXG_VARIANT: rx kernel variants (rxg_kernels_exp.hip)
-    int nocount = 0;     // RXG_NOCOUNT: skip the counter reduction
-    int pg_variant = 0;  // RXG_PG_VARIANT: payload-gather variants
-    int mirror_rebuild = 0;  // RXG_MIRROR_REBUILD: every mirror sync a full rebuild (round 1)
-    int replay_coarse = 0;   // RXG_REPLAY_COARSE: a write stales every later TCP packet on
-                             // its dport and all fix-ups run on the GPU (round 1)
 
     // tcbs[] writes posted by other threads (rxg_tcb_post), applied by the rx thread
     rxg::MpscRing<rxg_tcb_op> posted{RXG_TCB_QUEUE_CAP};
@@ -125,11 +116,14 @@ struct rxg_ctx {
     // and a launch on `stream` carries the burst's patch list itself (launch_bursts: no patch
     // launch before it); defer_patch asks apply_patches for that, ip_* is the list taken.
     bool patch_dev = false;
-    bool launch_patches = true;  // (experiment build: RXG_LAUNCH_PATCHES=0 turns the carrying off)
     bool defer_patch = false;
     const rxg::MirrorPatch *ip_list = nullptr;
     uint32_t ip_n = 0;
     int ip_buf = -1;
+    uint32_t ip_tables = 0;  // 1 << target of every patch in the carried list (rxg_mirror.h)
+    // HDP_MEM_COHERENCY_FLUSH_CNTL (hipDeviceProp_t::hdpMemFlushCntl; null if the runtime
+    // gives none): host writes through the BAR are flushed to memory before a kernel reads them
+    volatile uint32_t *hdp_flush = nullptr;
 
     unsigned long long *counters = nullptr;
     // the replays' counter corrections not yet on the device: added by the next mirror patch
@@ -251,6 +245,13 @@ struct rxg_ctx {
 // patch lists longer than this go through their own launch (every workgroup of a launch that
 // carries a list stores all of it)
 inline constexpr uint32_t kLaunchPatchMax = 256;
+
+// Host stores into device memory through the BAR (write-combined), made visible to the next
+// kernel: the CPU's write-combining buffers drained (sfence), the GPU's HDP write path flushed
+// (its flush register), then a read of the last word written -- a PCIe read completes only
+// after every posted write before it, the flush among them (the ROCm runtime's own recipe
+// for kernel arguments in device memory).  `last` NULL: no readback.
+void bar_publish(const rxg_ctx *c, const volatile uint32_t *last);
 
 inline constexpr size_t kCounterBytes = (size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS * sizeof(uint64_t);
 

@@ -43,6 +43,16 @@ int fail(int code, const char *fmt, ...)
 
 extern "C" const char *rxg_last_error(void) { return g_err; }
 
+void bar_publish(const rxg_ctx *c, const volatile uint32_t *last)
+{
+    _mm_sfence();
+    if (c->hdp_flush) {
+        *c->hdp_flush = 1u;
+        _mm_sfence();
+    }
+    if (last) (void)*last;
+}
+
 extern "C" int rxg_abi_version(void) { return RXG_ABI_VERSION; }
 
 extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
@@ -86,6 +96,8 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
             (void)hipFree(probe);
             c->patch_dev = true;
         }
+        hipDeviceProp_t hp;
+        if (hipGetDeviceProperties(&hp, c->device) == hipSuccess) c->hdp_flush = hp.hdpMemFlushCntl;
     }
     if (cfg) {
         c->replay_on_device = (cfg->flags & RXG_CFG_REPLAY_ON_DEVICE) != 0;
@@ -93,18 +105,6 @@ extern "C" int rxg_init(const rxg_config *cfg, rxg_ctx **out)
         c->max_blocks = cfg->max_blocks;
         if (cfg->zc_bytes) c->zc_bytes = cfg->zc_bytes;
     }
-#ifdef RXG_EXPERIMENTS
-    if (const char *g = getenv("RXG_MAX_BLOCKS")) c->max_blocks = (uint32_t)atoi(g);
-    if (const char *v = getenv("RXG_VARIANT")) c->variant = atoi(v);
-    if (const char *v = getenv("RXG_NOCOUNT")) c->nocount = atoi(v);
-    if (const char *v = getenv("RXG_PG_VARIANT")) c->pg_variant = atoi(v);
-    if (const char *v = getenv("RXG_ZC_BYTES")) c->zc_bytes = strtoull(v, nullptr, 10);
-    if (const char *v = getenv("RXG_MIRROR_REBUILD")) c->mirror_rebuild = atoi(v);
-    if (const char *v = getenv("RXG_REPLAY_COARSE")) c->replay_coarse = atoi(v);
-    if (const char *v = getenv("RXG_LAUNCH_PATCHES")) c->launch_patches = atoi(v) != 0;
-    if (const char *v = getenv("RXG_MIRROR_LOAD_PCT")) c->mir.max_load_pct = (uint32_t)atoi(v);
-    if (c->replay_coarse) c->replay_on_device = true;
-#endif
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(-EIO, "rxg_init: hipStreamCreate failed");
@@ -396,7 +396,10 @@ static int launch_patch_list(rxg_ctx *c, int bi, uint32_t n)
     pb.set = true;
     HIP_OK(hipEventRecord(c->mirror_ev, c->stream));
     c->mirror_ev_set = true;
-    c->mirror_ev_stale = false;
+    // a list a burst is still to carry (this launch was another table's overflow,
+    // apply_patches) is written after this recording: the event is re-recorded after that
+    // burst (mirror_event), as the rebuild paths do
+    c->mirror_ev_stale = c->ip_n != 0;
     return 0;
 }
 
@@ -409,16 +412,22 @@ static int apply_patches(rxg_ctx *c, M &mirror)
     const std::vector<MirrorPatch> &p = mirror.patches;
     if (p.empty()) return 0;
     const uint32_t n = (uint32_t)p.size();
+    uint32_t tables = 0;
+    for (const MirrorPatch &q : p) tables |= 1u << q.target;
     if (c->defer_patch && c->ip_n != 0) {
         // a second table's patches (the ARP mirror's after the TCB mirror's) join the list
-        // the burst carries, when it has room (the kernel applies each by its target)
+        // the burst carries, when it has room (the kernel applies each by its target).  Every
+        // workgroup of the carrying launch stores the whole list in parallel, so no two of its
+        // patches may write one word: a mirror emits at most one patch per word, and only a
+        // list for tables the carried one does not touch joins it.
         rxg_ctx::PatchBuf &cb = c->patch[c->ip_buf];
-        if (c->ip_n + n <= kLaunchPatchMax && c->ip_n + n <= cb.cap) {
+        if ((c->ip_tables & tables) == 0 && c->ip_n + n <= kLaunchPatchMax && c->ip_n + n <= cb.cap) {
             std::memcpy(cb.h + c->ip_n, p.data(), (size_t)n * sizeof(MirrorPatch));
-            if (c->patch_dev) _mm_sfence();
+            bar_publish(c, &cb.h[c->ip_n + n - 1].v[3]);
             mirror.patches_taken();
             ++c->table_writes;
             c->ip_n += n;
+            c->ip_tables |= tables;
             return 0;
         }
     }
@@ -440,13 +449,14 @@ static int apply_patches(rxg_ctx *c, M &mirror)
         pb.cap = cap;
     }
     std::memcpy(pb.h, p.data(), (size_t)n * sizeof(MirrorPatch));
-    if (c->patch_dev) _mm_sfence();  // write-combined through the BAR: out before the launch
+    if (c->patch_dev) bar_publish(c, &pb.h[n - 1].v[3]);  // through the BAR: out before the launch
     mirror.patches_taken();
     ++c->table_writes;
     if (c->defer_patch && c->ip_n == 0 && n <= kLaunchPatchMax) {
         c->ip_list = pb.h;
         c->ip_n = n;
         c->ip_buf = bi;
+        c->ip_tables = tables;
         c->mirror_ev_set = true;
         c->mirror_ev_stale = true;  // the carrying launch is the write (mirror_event)
         return 0;
@@ -481,7 +491,6 @@ int tcb_push(rxg_ctx *c)
     int rc = set_device(c);
     if (rc) return rc;
     TcbMirror &m = c->mir;
-    if (c->mirror_rebuild) m.need_rebuild = true;  // experiment build only
     if (m.need_rebuild) {
         m.rebuild();
         const size_t sb = m.slots.size() * sizeof(Slot), lb = m.listen.size() * sizeof(int32_t);
@@ -737,22 +746,6 @@ int begin_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, ui
     return 0;
 }
 
-// A receive launch: the product kernels, or in the experiment library the ablation kernels
-// of RXG_VARIANT (rxg_kernels_exp.hip).
-static hipError_t rx_launch(const rxg_ctx *c, const LaunchRx &L, hipStream_t st)
-{
-#ifdef RXG_EXPERIMENTS
-    if (c->variant) {
-        LaunchRx X = L;
-        X.variant = c->variant;
-        return launch_rx_exp(X, st);
-    }
-#else
-    (void)c;
-#endif
-    return launch_rx(L, st);
-}
-
 static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bursts, uint32_t k, uint32_t rec_kind,
                          void *stream, const char *who, uint32_t stride64 = 0,
                          const rxg_payload_slots *pay = nullptr)
@@ -772,7 +765,7 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
     for (uint32_t j = 0; j < std::min(k, kMaxBursts); ++j) first_has_frames |= bursts[j].n != 0;
     bool others_pending = false;
     for (const auto &r : c->readers) others_pending |= r.pending;
-    c->defer_patch = c->launch_patches && c->patch_dev && st == c->stream && first_has_frames && !others_pending;
+    c->defer_patch = c->patch_dev && st == c->stream && first_has_frames && !others_pending;
     int rc = begin_bursts(c, frames, bursts, k, rec_kind, who, stride64);
     c->defer_patch = false;
     if (rc) {
@@ -798,7 +791,7 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
             L.pay_arena = (uint8_t *)pay->arena;
             L.pay_msgs = pay->msgs;
         }
-        L.counters = c->nocount ? nullptr : c->counters;
+        L.counters = c->counters;
         // (the by-reference hand-off writes no payload: its kernel's occupancy grid)
         L.max_blocks = c->max_blocks ? c->max_blocks : pay && pay->arena ? c->grid_pay
                      : pay ? (rec_kind == RXG_REC48 ? c->grid_ref48 : rec_kind == RXG_REC8 ? c->grid_ref8 : c->grid_ref16)
@@ -809,7 +802,7 @@ static int launch_bursts(rxg_ctx *c, const void *frames, const rxg_dev_burst *bu
             L.ipatch = c->ip_list;
             L.nipatch = c->ip_n;
         }
-        const hipError_t e = rx_launch(c, L, st);
+        const hipError_t e = launch_rx(L, st);
         if (e != hipSuccess) {
             (void)launch_carried_patches(c);
             HIP_OK(e);

@@ -33,9 +33,8 @@ struct LaunchRx {
     uint32_t stride64;     // nonzero: frame i of a burst at slot slot0 + i * stride64 (no off64[])
     uint8_t *pay_arena;    // non-null (with pay_msgs): the payload hand-off fused in (one burst,
     rxg_payload_msg *pay_msgs;  //   record kind 8 / 16 / 48; rxg_rx_burst_payload_dev)
-    int variant;           // experiment library only (launch_rx_exp): RXG_VARIANT
     // mirror patches the launch applies before its first probe, in place of a patch launch
-    // before it (rxg_host.cpp launch_bursts; the list in device memory, kInlinePatchMax at most)
+    // before it (rxg_host.cpp launch_bursts; the list in device memory, kLaunchPatchMax at most)
     const MirrorPatch *ipatch;
     uint32_t nipatch;
 };
@@ -65,15 +64,9 @@ struct LaunchPayload {
     unsigned long long ticket_base;   // its value before this launch
     unsigned long long *used;         // 1 entry
     uint32_t epoch;                   // 1 .. 2^30-1, new for every launch on `status`
-    int variant;                      // 0 = production; >0 experiment variants (RXG_PG_VARIANT)
 };
 
 hipError_t launch_rx(const LaunchRx &L, hipStream_t st);
-#ifdef RXG_EXPERIMENTS
-// rxg_kernels_exp.hip (experiment library only): the experiment kernels of L.variant;
-// hipErrorInvalidValue for a variant it does not know
-hipError_t launch_rx_exp(const LaunchRx &L, hipStream_t st);
-#endif
 
 // Latency mode (rxg_server_*): a persistent set of workgroups that classifies one burst after
 // another.  The host posts a request in a mailbox of fine-grained (coherent) host memory and

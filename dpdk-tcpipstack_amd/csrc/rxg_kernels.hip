@@ -1,8 +1,7 @@
 // rxg_kernels.hip — the product kernels of librxg.so (gfx950): the receive / tx-checksum
 // kernels instantiated from rxg_rx.h (one per record kind, descriptor form, burst count and
 // prefetch depth), the latency-mode server, the synthetic-frame generator, the mirror patch
-// and the counter corrections, and their launch wrappers.  No experiment variant lives here:
-// the ablation kernels are rxg_kernels_exp.hip, built into librxg_exp.so only.
+// and the counter corrections, and their launch wrappers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

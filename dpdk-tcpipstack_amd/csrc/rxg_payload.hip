@@ -611,35 +611,10 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     *launched = 0;
     hipError_t e = hipMemsetAsync(P.used, 0, sizeof(unsigned long long), st);
     if (e != hipSuccess || P.n == 0) return e;
-#ifdef RXG_EXPERIMENTS
-    const int variant = P.variant;
-#else
-    const int variant = 0;
-#endif
-    const int fpt = (variant == 6 || variant == 7) ? 4 : 1;
-    // workgroup size of the kernel the switch below launches
-    const int tpb = (variant >= 1 && variant <= 10) ? kPgThreads : variant == 12 ? 512 : kPgThreadsProd;
-    a.nblocks = (P.n + tpb * fpt - 1) / (tpb * fpt);
-    const dim3 g(a.nblocks), b(tpb);
-#ifdef RXG_EXPERIMENTS
-    switch (variant) {  // experiment variants (RXG_PG_VARIANT, experiment library only)
-    case 1: hipLaunchKernelGGL((pg_gather<4, false, 1, true>), g, b, 0, st, a); break;
-    case 5: hipLaunchKernelGGL((pg_gather<4, true, 1, false>), g, b, 0, st, a); break;
-    case 6: hipLaunchKernelGGL((pg_gather<4, true, 4, true>), g, b, 0, st, a); break;
-    case 7: hipLaunchKernelGGL((pg_gather<4, true, 4, false>), g, b, 0, st, a); break;
-    case 8: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 0>), g, b, 0, st, a); break;  // look-back first
-    case 9: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 1>), g, b, 0, st, a); break;  // one set early
-    case 10: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 256>), g, b, 0, st, a); break;
-    case 11: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 1024>), g, b, 0, st, a); break;
-    case 12: hipLaunchKernelGGL((pg_gather<4, true, 1, true, 2, 512>), g, b, 0, st, a); break;
-    // 13: production without the frame header-word load (timing only: data_off taken as 5)
-    case 13: hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd, false>), g, b, 0, st, a); break;
-    default: hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
-    }
-#else
+    a.nblocks = (P.n + kPgThreadsProd - 1) / kPgThreadsProd;
+    const dim3 g(a.nblocks), b(kPgThreadsProd);
     hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
-#endif
-    *launched = (a.ticket && (variant != 5 && variant != 7)) ? a.nblocks : 0u;
+    *launched = a.ticket ? a.nblocks : 0u;
     return hipGetLastError();
 }
 

@@ -71,7 +71,6 @@ extern "C" int rxg_payload_gather_dev(rxg_ctx *c, const rxg_payload_out *o, void
     P.ticket_base = c->pg_tickets;
     P.used = (unsigned long long *)o->arena_used;
     P.epoch = c->pg_epoch;
-    P.variant = c->pg_variant;
     uint32_t tickets = 0;
     HIP_OK(launch_payload(P, st, &tickets));
     c->pg_tickets += tickets;
@@ -294,8 +293,6 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
             }
             filt[(h >> 6) & 1023u] |= 1ull << (h & 63u);
         }
-        if (c->replay_coarse)  // experiment build only: the round-1 rule, any packet on the dport
-            for (const TupleKey &k : keys) listen_seq.emplace_back(-1 - (int32_t)(k.ports >> 16), wseq);
         for (int32_t d : listen) {
             bool found = false;
             for (auto &e : listen_seq)
@@ -338,9 +335,6 @@ extern "C" int rxg_rx_replay(rxg_ctx *c, const rxg_handoff_ops *ops, void *const
             for (const auto &e : listen_seq)
                 if (e.first == d && e.second > s) return true;
         }
-        if (c->replay_coarse)
-            for (const auto &e : listen_seq)
-                if (e.first == -1 - d && e.second > s) return true;
         return false;
     };
     // writes the replays of this launch's earlier bursts made, then those since

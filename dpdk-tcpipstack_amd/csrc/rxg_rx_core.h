@@ -204,7 +204,8 @@ struct Rec {
 // The mirror patches a launch carries (LaunchRx::ipatch, in place of a mirror_patch launch
 // before it): every workgroup stores all of them before its first table read -- the same
 // values to the same words, so none needs another's (no grid-wide order), and each waits
-// for its own stores before its waves read the tables.  Few (kInlinePatchMax), by contract.
+// for its own stores before its waves read the tables.  At most kLaunchPatchMax, no two
+// to one word (rxg_host.cpp apply_patches), by contract.
 __device__ __forceinline__ void apply_launch_patches(const RxArgs &a)
 {
     uint4 *buckets = const_cast<uint4 *>(a.t.buckets);

@@ -35,7 +35,7 @@ int SrvPort::launch()
     L.mbox = S.mbox;
     L.ret = S.ret;
     L.ctl = S.ctl;
-    L.counters = c->nocount ? nullptr : c->counters;
+    L.counters = c->counters;
     L.idle_ticks = S.idle_ticks;
     L.blocks = S.blocks;
     L.mode = (int)S.rec_kind;
@@ -68,7 +68,9 @@ void SrvPort::request_stop()
 void SrvPort::write(unsigned long long q)
 {
     rxg_ctx::Server &S = c->srv;
-    _mm_sfence();
+    // the staging (device memory: through the BAR and the HDP) flushed before the request
+    if (S.dev) bar_publish(c, nullptr);
+    else _mm_sfence();
     const bool inl = (S.req.flags & kSrvInlineDesc) != 0u;
     const unsigned long long ck = srv_check(q, S.req, inl ? S.idesc : nullptr);
     if (S.mdev) {

@@ -13,11 +13,9 @@
 #   prof        rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes per workload
 #               (scripts/gpu_prof.sh; PROF_WLS, default "c3 c4 c2 c2multi"; REC, default 8)
 #   sq          SQ counter passes per workload (scripts/gpu_sq.sh; SQ_WLS)
-#   ab          in-process kernel A/B, records checked (scripts/gpu_ab.sh; VARIANTS, WLS comma-separated)
 #   crossover   small-burst crossover against the reference CPU path (scripts/crossover.py)
 #   group       group-burst latency (scripts/grouplat.py)
 #   churn       burst + replay under SYN/FIN churn (scripts/churnbench.sh)
-#   pg          payload-gather A/B (scripts/pgbench.py; PG_VARIANTS)
 set -u
 TAG=${1:?usage: gpu_check.sh TAG STEP...}; shift
 OUT=gpurun_out/$TAG
@@ -45,11 +43,9 @@ for S in "$@"; do
     rehearse)  step rehearse2 600 env RXG_BENCH_REHEARSE=1 python3 -u bench.py --gpus 2 --steps 20 --warmup 3 ;;
     prof)      step prof 900 env REC=${REC:-8} bash scripts/gpu_prof.sh "$TAG/prof" ${PROF_WLS:-c3 c4 c2 c2multi} ;;
     sq)        step sq 600 env REC=${REC:-8} bash scripts/gpu_sq.sh ${SQ_WLS:-c4 c3} ;;
-    ab)        step ab 800 env TAG="$TAG/ab" bash scripts/gpu_ab.sh ;;
     crossover) step crossover 500 python3 -u scripts/crossover.py ;;
     group)     step grouplat 200 python3 -u scripts/grouplat.py ;;
     churn)     step churn 600 bash scripts/churnbench.sh "$OUT/churn.jsonl" ;;
-    pg)        step pg 500 env TAG="$TAG/pg" VARIANTS=${PG_VARIANTS:-0} bash scripts/gpu_pg.sh ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done

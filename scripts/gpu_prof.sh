@@ -19,11 +19,12 @@ for W in "$@"; do
     pr*) K="rx_kernel<$REC, 0, false, false, 2>" ;;
     *)   K="rx_kernel<$REC," ;;
   esac
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $CMD > $O/trace.log 2>&1 || { echo "STOP trace $W"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- $CMD > $O/fetch.log 2>&1 || { echo "STOP fetch $W"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- $CMD > $O/write.log 2>&1 || { echo "STOP write $W"; exit 1; }
+  # each run writes the build it loaded (src= hash): the trace directory and traffic.json name it
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $CMD --prov $O/build_trace.json > $O/trace.log 2>&1 || { echo "STOP trace $W"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- $CMD --prov $O/build_fetch.json > $O/fetch.log 2>&1 || { echo "STOP fetch $W"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- $CMD --prov $O/build_write.json > $O/write.log 2>&1 || { echo "STOP write $W"; exit 1; }
   F=$(ls $O/fetch/*counter_collection.csv | head -1); Wr=$(ls $O/write/*counter_collection.csv | head -1)
-  python3 scripts/pmc_traffic.py "$F" "$Wr" "$K" $O/traffic.json "$CMD" > /dev/null || { echo "STOP traffic $W"; exit 1; }
+  python3 scripts/pmc_traffic.py "$F" "$Wr" "$K" $O/traffic.json "$CMD" --prov $O/build_trace.json $O/build_fetch.json $O/build_write.json > /dev/null || { echo "STOP traffic $W"; exit 1; }
   echo "$W ok"
 done
 echo done

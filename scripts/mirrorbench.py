@@ -3,11 +3,9 @@
 
 For Ntcb = 1 001 / 65 537 / 1 048 577 (C3 / C4 / C5 tables): k writes (half tcp_listen
 children appended at Ntcb, half remove_tcb of random flows), then rxg_tcb_sync and a stream
-sync; host wall time per sync, per write.  Run once with the product library (O(1) device
-patches) and once with the experiment library under RXG_MIRROR_REBUILD=1 (round 1: every
-sync rebuilds and uploads the whole table):
-  python scripts/mirrorbench.py            # product
-  RXG_LIB_OVERRIDE=1 RXG_LIB=dpdk-tcpipstack_amd/rxg/librxg_exp.so RXG_MIRROR_REBUILD=1 python scripts/mirrorbench.py
+sync; host wall time per sync, per write, with the product library (O(1) device patches; round
+1's full rebuild per sync was measured through the retired experiment library, HISTORY.md):
+  python scripts/mirrorbench.py
 Prints one JSON line per (Ntcb, k)."""
 import json
 import os
@@ -25,7 +23,7 @@ import rxg  # noqa: E402
 
 def main():
     eng = rxg.Engine(0)
-    mode = "rebuild" if os.environ.get("RXG_MIRROR_REBUILD") == "1" else "patch"
+    mode = "patch"
     rng = random.Random(1)
     dst = rxg.ip_raw(192, 168, 78, 2)
     for nflows in (1000, 65536, 1 << 20):
@@ -35,7 +33,7 @@ def main():
         eng.sync()
         n = nflows + 1
         for k in (1, 32, 1024):
-            reps = 30 if (mode == "rebuild" and nflows == 1 << 20) else 100
+            reps = 100
             ts = []
             for _ in range(reps):
                 t0 = time.perf_counter()

@@ -7,11 +7,30 @@ FETCH_SIZE reports exactly half the bytes of a wide (16 B/lane) coalesced stream
 so it is doubled; WRITE_SIZE is exact for 16 B/lane stores and for atomics.
 
   python scripts/pmc_traffic.py <fetch_csv> <write_csv> <kernel-substring> <out.json> [note]
+         [--prov build_fetch.json build_write.json ...]
+
+--prov: the build provenance each counted run wrote (scripts/profrun.py --prov).  They must
+name one src= hash; it is stamped into out.json ("build", "source_hash"), which bench.py
+compares with the library it loaded (roofline.traffic_matches_build).
 """
 import csv
 import json
 import statistics
 import sys
+
+
+def src_of(build: str):
+    """The src= hash of an rxg_build_info() string, or None."""
+    return next((w[4:] for w in (build or "").split() if w.startswith("src=")), None)
+
+
+def stamp(prov_files):
+    """The one build the counted runs loaded: {"build", "source_hash"}; ValueError if they differ."""
+    builds = [json.load(open(p))["build"] for p in prov_files]
+    srcs = {src_of(b) for b in builds}
+    if len(srcs) != 1 or None in srcs:
+        raise ValueError(f"counted runs loaded different or unstamped builds: {sorted(map(str, srcs))}")
+    return {"build": builds[0], "source_hash": srcs.pop()}
 
 
 def per_launch(path, kernel):
@@ -21,8 +40,13 @@ def per_launch(path, kernel):
 
 
 def main():
-    fetch_csv, write_csv, kernel, out = sys.argv[1:5]
-    note = sys.argv[5] if len(sys.argv) > 5 else ""
+    argv = sys.argv[1:]
+    prov = []
+    if "--prov" in argv:
+        k = argv.index("--prov")
+        argv, prov = argv[:k], argv[k + 1:]
+    fetch_csv, write_csv, kernel, out = argv[:4]
+    note = argv[4] if len(argv) > 4 else ""
     f = per_launch(fetch_csv, kernel)
     w = per_launch(write_csv, kernel)
     read_b = 2.0 * statistics.median(f) * 1024.0
@@ -33,6 +57,8 @@ def main():
            "hbm_bytes_per_launch": read_b + write_b,
            "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16 B/lane streams); "
                          "write = WRITE_SIZE x 1024", "note": note}
+    if prov:
+        res.update(stamp(prov))
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 

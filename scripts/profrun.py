@@ -2,7 +2,11 @@
 """A fixed number of rx launches of one bench workload through the product library, for
 rocprofv3 (kernel trace / PMC passes): scripts/gpu_prof.sh.  The same synthetic batches,
 tables and launch forms as bench.py; no timing of its own.
-  python scripts/profrun.py --workload c2multi --iters 20 [--rec 8]"""
+  python scripts/profrun.py --workload c2multi --iters 20 [--rec 8] [--prov build.json]
+
+--prov writes rxg.build_provenance() of the library this process loaded (its src= hash) to a
+file: scripts/gpu_prof.sh stamps every traffic.json and kernel-trace directory with it."""
+import json
 import argparse
 import os
 import sys
@@ -24,9 +28,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rec", type=int, default=16, choices=[8, 16, 48])
+    ap.add_argument("--prov", default=None, help="write the loaded library's build provenance here")
     args = ap.parse_args()
     rec = args.rec
     eng = rxg.Engine(0)
+    if args.prov:
+        with open(args.prov, "w") as fh:
+            json.dump(rxg.build_provenance(), fh, indent=1)
     n = args.frames
     if args.workload in ("c2multi", "c2multis"):  # bench.py multiburst_leg: 16 bursts of one 1 GiB pool per launch
         k = 16

@@ -78,3 +78,32 @@ def test_pg_backend_choice():
     assert bench.pg_backend("auto", 2, True) == "gloo"
     assert bench.pg_backend("nccl", 1, False) == "nccl"
     assert bench.SOLO_BUDGET_S < 900.0 / 3  # the solo legs end well inside the default timeout
+
+
+def test_traffic_provenance_reports_a_mismatched_build(tmp_path):
+    """roofline.traffic names the build its PMC passes counted
+    (scripts/pmc_traffic.py --prov stamps the src= hash), and the line says whether that is
+    the library it measured.  A file from another build, or an unstamped one, reports
+    traffic_matches_build false."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench
+    import pmc_traffic
+    built = "rxg src=0123456789abcdef rev=abc built=x gfx950"
+    for name, stamped, ok in [("same", "0123456789abcdef", True), ("other", "fedcba9876543210", False),
+                              ("unstamped", None, False)]:
+        tf = tmp_path / f"{name}.json"
+        d = {"hbm_bytes_per_launch": 1.0}
+        if stamped:
+            d["source_hash"] = stamped
+        tf.write_text(json.dumps(d))
+        p = bench.traffic_provenance(str(tf), built)
+        assert p["traffic_matches_build"] is ok and p["traffic_src"] == stamped and p["build_src"] == "0123456789abcdef"
+    assert bench.traffic_provenance(None, built)["traffic_matches_build"] is False
+    # the stamp: one build across the counted runs, else refused
+    a, b = tmp_path / "a.json", tmp_path / "b.json"
+    a.write_text(json.dumps({"build": built}))
+    b.write_text(json.dumps({"build": built.replace("0123", "9999")}))
+    assert pmc_traffic.stamp([str(a), str(a)]) == {"build": built, "source_hash": "0123456789abcdef"}
+    with pytest.raises(ValueError):
+        pmc_traffic.stamp([str(a), str(b)])

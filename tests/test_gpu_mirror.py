@@ -340,3 +340,73 @@ def test_carried_patches_then_a_burst_on_another_stream(engine):
         for v in dev.values():
             if isinstance(v, rxg.DevArray):
                 v.free()
+
+
+@pytest.mark.parametrize("reader", ["stream", "server"])
+@pytest.mark.parametrize("narp", [300, 250])
+def test_carried_list_then_an_overflowing_arp_list(reader, narp):
+    """a TCB list the burst on the context's stream carries, then an ARP list
+    that does not fit beside it (narp alone past kLaunchPatchMax = 256, or the sum past it)
+    and so goes through its own patch launch before that burst.  The next table reader -- a
+    burst on a caller stream, or a served burst (rxg_server_burst_dev) -- must wait for the
+    carrying burst, not for the event recorded after the ARP launch (csrc/rxg_host.cpp
+    launch_patch_list: the event stays stale while a list is still to be carried).  A long
+    burst on the context's stream runs first, so the ARP launch, the carrying burst and the
+    reader all queue behind it.  Checked against the synthetic flows and the oracle's ARP set
+    (arp.c:282-317: a learned source is no longer flagged)."""
+    eng = rxg.Engine(device=0)
+    n, nflows, m = 1 << 20, 1000, 4096
+    dev = eng.synth(n=n, nflows=nflows, len_a=1500, seed=606, with_flows=True)
+    t0, l0 = rxg.synthetic_tcb_table(nflows)
+    srcs = t0["ipv4_src"][1:]
+    flows = dev["flow"].download(np.uint32, n)
+    out_a, out_b, out_r = eng.alloc(n * 16), eng.alloc(n * 16), eng.alloc(n * 16)
+    s2 = torch.cuda.Stream()
+    # never-seen addresses fill the ARP list past the join's room; the flows' own sources
+    # (half of them) are learned in the same list
+    extra = [pktgen.ip4(100, 64, i >> 8, i & 255) for i in range(narp - nflows // 2 if narp > nflows // 2 else 0)]
+    try:
+        if reader == "server":
+            eng.server_start(rxg.REC16, blocks=4, max_frames=m)
+        for rnd in range(3):
+            eng.tcb_load(t0, l0)
+            eng.arp_load([pktgen.ip4(99, 0, i >> 8, i & 255) for i in range(1200)])  # sized: no rebuild below
+            eng.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, m, out_r.ptr, 16, None)
+            eng.sync()
+            torch.cuda.synchronize()
+            eng.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out_a.ptr, 16, None)  # long
+            removed = sorted(set(range(1 + rnd, nflows + 1, 97)))  # ~10 removals: a carried list
+            for i in removed:
+                eng.tcb_remove(i)
+            learned = [int(x) for x in srcs[rnd % 2::2][:min(narp, nflows // 2)]] + extra
+            learned = learned[:narp]
+            for ip in learned:
+                eng.arp_learned(ip)
+            eng.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out_b.ptr, 16, None)  # carries
+            if reader == "stream":
+                eng.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out_r.ptr, 16, s2.cuda_stream)
+                k = n
+            else:
+                eng.server_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, m, out_r.ptr, rxg.REC16)
+                k = m
+            torch.cuda.synchronize()
+            eng.sync()
+            gone = np.isin(flows.astype(np.int64) + 1, removed)
+            known = np.isin(srcs[flows], np.asarray(learned, dtype=srcs.dtype))
+            a = out_a.download(rxg.REC16_DTYPE, n)
+            assert (a["tcb_idx"] == flows.astype(np.int32) + 1).all(), "the first burst saw later writes"
+            for o, kk in ((out_b, n), (out_r, k)):
+                r = o.download(rxg.REC16_DTYPE, kk)
+                g, kn, f = gone[:kk], known[:kk], flows[:kk]
+                assert (r["tcb_idx"][~g] == f[~g].astype(np.int32) + 1).all(), (rnd, "stale TCB entry")
+                assert (r["tcb_idx"][g] == 0).all() and (r["verdict"][g] == rxg.V_RST_LISTEN_NONSYN).all(), rnd
+                assert ((r["flags"] & rxg.F_ARP_LEARN) != 0).tolist() == (~kn).tolist(), (rnd, "stale ARP entry")
+        if reader == "server":
+            eng.server_stop()
+    finally:
+        for d in (out_a, out_b, out_r):
+            d.free()
+        for v in dev.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()
+        eng.close()
