@@ -605,6 +605,40 @@ def small_burst_leg(gpu, n=32, seconds=0.3):
     return res
 
 
+def host_cpus() -> dict:
+    """The host the CPU baseline runs on: the CPU model, nproc, this
+    process's affinity, and the cgroup CPU quota (cpu.max) when one is set -- on the GPU box
+    nproc and the affinity show the whole machine while the job's share is smaller.  `usable`
+    = the affinity, capped by that share: the replica leg's core count."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    # the job's CPU share: the cgroup quota, else the thread budget the job was given
+    # (OMP_NUM_THREADS: 16 per GPU on the GPU box, whose affinity spans the whole machine)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if quota is not None:
+        usable, why = max(1, min(aff, int(quota))), "cgroup cpu.max quota"
+    elif omp.isdigit() and int(omp) > 0:
+        usable, why = min(aff, int(omp)), "OMP_NUM_THREADS (the job's thread budget)"
+    else:
+        usable, why = aff, "affinity"
+    return {"model": model, "nproc": os.cpu_count(), "affinity": aff,
+            "cgroup_quota_cpus": round(quota, 2) if quota is not None else None,
+            "omp_num_threads": int(omp) if omp.isdigit() else None, "usable": usable, "usable_from": why}
+
+
 def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
     """The oracle's faithful restatement of the reference rx path (port), on one host
     core, over a bounded sample of the same workload (first sample_n frames)."""
@@ -632,10 +666,13 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
             s = 0 if e >= n else e
         dt = time.perf_counter() - t0
         res[opt] = (pk / dt / 1e6, by / dt / 1e9, pk, dt)
+        arp_entries = oracle.arp_count(opt)  # the list each packet's get_mac walks (ip.c:26-32)
     oracle.arp_reset()
     mpps0, gbs0, pk0, dt0 = res["O0"]
     mpps2, gbs2, pk2, dt2 = res["O2"]
     multi = cpu_replicas(arena, off, lens, tcb, live, cores, seconds * 0.5) if cores > 1 else None
+    if multi:
+        multi["per_core_over_1core_O0"] = round(multi["mpps"] / multi["cores"] / mpps0, 3)
     # SURVEY.md §6 timed the reference's own hot-path files on this shape (1 500 B, 1 000 flows /
     # 1 000 source IPs, +verify) in the survey's container: 0.0121 Mpps at -O0, 0.0185 at -O2.
     # The port, timed on the same shape in the same container class (scripts/cpu_calib.py,
@@ -654,7 +691,7 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
                  "reference_equivalent": {"O0_mpps": round(mpps0 * f0, 6), "O0_gbs": round(gbs0 * f0, 6),
                                           "O2_mpps": round(mpps2 * f2, 6), "O2_gbs": round(gbs2 * f2, 6)}}
     return {"value": round(gbs0, 6), "unit": "GB/s", "mpps": round(mpps0, 6), "cores": 1,
-            "kind": "port",
+            "kind": "port", "host": host_cpus(), "arp_entries": arp_entries,
             "sample": (f"faithful oracle (reference algorithms: byte-loop checksum, malloc+memcpy "
                        f"pseudo header, two-pass linear findtcb over {wl.flows + 1} TCBs, ARP list "
                        f"walks, disabled-logger calls) built -O0 like tcp_ip_stack/Makefile:50, "
@@ -712,8 +749,12 @@ def cpu_replicas(arena, off, lens, tcb, live, cores, seconds):
         return None
     mpps = sum(o["frames"] / o["seconds"] for o in outs) / 1e6
     gbs = sum(o["bytes"] / o["seconds"] for o in outs) / 1e9
+    arp = sorted({o["arp_entries"] for o in outs})
     return {"cores": cores, "mpps": round(mpps, 6), "gbs": round(gbs, 6), "opt": "O0",
-            "sample": f"{cores} processes, frames split {cuts[1] - cuts[0]}-ish each, {seconds:.1f} s"}
+            "arp_entries": arp[0] if len(arp) == 1 else arp,
+            "sample": f"{cores} processes (one per usable core: host.usable), frames split "
+                      f"{cuts[1] - cuts[0]}-ish each, each after an untimed pass over the whole sample "
+                      f"(its ARP list = the 1-core leg's), {seconds:.1f} s"}
 
 
 def _free_port() -> int:
@@ -949,7 +990,7 @@ def main():
     # driver's N > 1 lines carry null; the other ranks would only wait at the barrier).
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        cores = args.cpu_cores or host_cpus()["usable"]
         cpu = cpu_baseline(eng, wl, seconds=args.cpu_seconds, cores=cores)
     barrier(device)
 

@@ -96,3 +96,8 @@ def tx_batch(arena, off64, lens):
 def arp_reset():
     lib().orc_arp_reset()
     lib("O0").orc_arp_reset()
+
+
+def arp_count(opt: str = "O0") -> int:
+    """Entries in the faithful path's ARP list (arp.c:282-317 add_mac) of the given build."""
+    return int(lib(opt).orc_arp_count())

@@ -3,6 +3,11 @@
 //   flat:  contiguous source
 //   rows:  2^20 rows of 1 456 B at a 1 536 B stride (C3's payload spans, 16-byte aligned;
 //          the gather also shifts each row by 6 bytes) -> contiguous destination
+//   slotsWL: 2^20 slots of 1 536 B (a C3 frame's 24 lines): every line read, the first WL
+//          written to the same slot of a second pool -- the fused copy hand-off's traffic with
+//          whole-line writes, WL = 24 as shipped (the payload at its pool offset: header line
+//          and slot tail written) against WL = 23 (a 1 446 B payload from its first byte at the
+//          slot's start: DESIGN.md §4.F's line-aligned estimate)
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/copybw scripts/copybw.hip
 // Run:   build/copybw [workgroups per CU ...]   (default 2 4 8)
 #include <hip/hip_runtime.h>
@@ -54,6 +59,26 @@ __global__ __launch_bounds__(256) void rows(const u32x4 *src, u32x4 *dst, size_t
     }
 }
 
+// chunk k of slot r: read always, written when it lies in the slot's first WL lines
+template <int WL, int U>
+__global__ __launch_bounds__(256) void slots(const u32x4 *src, u32x4 *dst, size_t n16)
+{
+    const size_t stride = (size_t)gridDim.x * 256u * U;
+    for (size_t i = (size_t)blockIdx.x * 256u * U + threadIdx.x; i < n16; i += stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t k = i + 256u * u;
+            if (k < n16) v[u] = __builtin_nontemporal_load(src + k);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t k = i + 256u * u;
+            if (k < n16 && (k % 96u) < WL * 4u) __builtin_nontemporal_store(v[u], dst + k);
+        }
+    }
+}
+
 template <typename K>
 static float run(K kern, int grid, const u32x4 *s, u32x4 *d, size_t n16)
 {
@@ -84,6 +109,9 @@ int main(int argc, char **argv)
     CK(hipMalloc(&src, nrows * 1536u));
     CK(hipMalloc(&dst, n16 * 16u));
     CK(hipMemset(src, 1, nrows * 1536u));
+    u32x4 *pool2;
+    CK(hipMalloc(&pool2, nrows * 1536u));
+    const size_t s16 = nrows * 96u;
     int ncu = 0;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     std::vector<int> wpc = {2, 4, 8};
@@ -100,6 +128,15 @@ int main(int argc, char **argv)
         for (auto &x : r)
             printf("{\"copy\": \"%s\", \"wg_per_cu\": %d, \"us_median\": %.1f, \"bytes_moved\": %.0f, \"TBps\": %.3f}\n",
                    x.name, w, x.us, bytes, bytes / x.us / 1e6);
+        struct { const char *name; int wl; float us; } q[] = {
+            {"slots24", 24, run(slots<24, 4>, g, src, pool2, s16)},
+            {"slots23", 23, run(slots<23, 4>, g, src, pool2, s16)},
+        };
+        for (auto &x : q) {
+            const double b = (double)nrows * (1536.0 + 64.0 * x.wl);
+            printf("{\"copy\": \"%s\", \"wg_per_cu\": %d, \"us_median\": %.1f, \"bytes_moved\": %.0f, \"TBps\": %.3f}\n",
+                   x.name, w, x.us, b, b / x.us / 1e6);
+        }
     }
     return 0;
 }
