@@ -677,7 +677,7 @@ def cpu_baseline(eng, wl, seconds=10.0, sample_n=20000, cores=1):
     # 1 000 source IPs, +verify) in the survey's container: 0.0121 Mpps at -O0, 0.0185 at -O2.
     # The port, timed on the same shape in the same container class (scripts/cpu_calib.py,
     # profiles/r05/cpu_calib/container.json), runs 1.37x (-O0) / 1.5x (-O2) slower; no slower
-    # construct was found in its code, and the reference cannot be built here
+    # construct was found in its code (HISTORY.md §6.R5), and the reference cannot be built here
     # (no DPDK headers) to time it on this host.  So the factor is stated, with the reference-
     # equivalent rate it implies: a GPU-over-CPU ratio against `value` is inflated by it.
     calib = None

@@ -14,7 +14,7 @@
 namespace rxg {
 
 // ---------------------------------------------------------------------------------------
-// Device TCB mirror (DESIGN.md §HBM layout).
+// Device TCB mirror.
 //   bucket table: nbuckets x 4 slots x 16 B = one 64-byte line per bucket.  A slot is
 //     {ports = dport<<16 | sport, ipv4_dst raw, ipv4_src host, value}; value = the
 //     LOWEST tcbs[] index holding that exact tuple (findtcb pass 1 returns the first

@@ -88,7 +88,7 @@ struct SrvReq {
 constexpr uint32_t kSrvInline = 32;
 constexpr uint32_t kSrvInlineDesc = 1u;
 // A host burst holding a frame over 64 bytes: a request of 3..gridDim slices then runs one
-// slice per workgroup, each shared by the workgroup's four waves (rx_body).
+// slice per workgroup, each shared by the workgroup's four waves (rx_body, HISTORY.md §9.R4).
 constexpr uint32_t kSrvLarge = 2u;
 // Device memory written through the BAR (large-BAR GPUs, whole lines per post) or coherent
 // host memory; `done` / `exited` are read from the server's return block (host memory, may

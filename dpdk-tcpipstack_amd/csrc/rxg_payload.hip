@@ -4,8 +4,8 @@
 // mempool message for the socket ring: tcp_established -> PushData (tcp_windows.c:341-358)
 // -> AdjustPair (:42-110) -> PushDataInQueue (:112-136) -> GetData (:138-186), whose
 // memcpy reads `Length` bytes at frame + 34 + tcp_len (:164-172; the IP header is taken
-// as 20 bytes whatever the IHL, like the parse).  rxg does that copy for a whole burst in
-// three launches:
+// as 20 bytes whatever the IHL, like the parse).  rxg does that copy for a whole burst
+// after it (rxg_rx_burst_payload_dev fuses it into the burst instead, rxg_rx_core.h):
 //
 //   pg_gather  ONE launch, 1 024 frames per workgroup: each workgroup sums its candidates'
 //              arena space (each payload rounded up to 16 bytes so that every message starts
@@ -35,12 +35,11 @@
 namespace rxg {
 namespace {
 
-constexpr int kPgThreads = 256;  // frames per workgroup of the smallest form (status words are sized for it)
-// production: 1 024 frames (16 waves) per workgroup, 2 copy rounds per set (80 VGPRs,
-// 6 waves per SIMD), DESIGN.md §5
-constexpr int kPgThreadsProd = 1024;
-constexpr int kPgRoundsProd = 2;
-constexpr int kMaxU = 4;         // copy rounds in flight per wave (max)
+constexpr int kPgThreads = 256;  // status words are sized for 256-frame workgroups (payload_blocks)
+// 1 024 frames (16 waves) per workgroup, 2 copy rounds per set (80 VGPRs, 6 waves per SIMD);
+// the other sizes and depths measured slower (HISTORY.md §5, "pg_gather")
+constexpr int kPgFrames = 1024;
+constexpr int kPgRounds = 2;
 constexpr uint32_t kSpinLimit = 1u << 22;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -70,7 +69,6 @@ struct Cand {
 };
 
 
-template <bool HDR = true>
 __device__ __forceinline__ Cand candidate(const PgArgs &a, uint32_t i)
 {
     Cand c{0ull, 0u, 0u};
@@ -102,8 +100,7 @@ __device__ __forceinline__ Cand candidate(const PgArgs &a, uint32_t i)
     if (verdict > RXG_V_RST_LISTEN_NONSYN || datalen <= 0 || (rflags & RXG_F_TRUNC)) return c;
     const uint64_t base = (uint64_t)off * 64u;
     // bytes 44..47 of the frame (>= 54 bytes: not RXG_F_TRUNC); data_off is byte 46
-    // (HDR false, experiment build only, timing: data_off taken as 5 without the load)
-    const uint32_t dw = HDR ? *reinterpret_cast<const uint32_t *>(a.frames + base + 44u) : 0x00500000u;
+    const uint32_t dw = *reinterpret_cast<const uint32_t *>(a.frames + base + 44u);
     const uint32_t start = RXG_OFF_TCP + ((dw >> 20) & 0xFu) * 4u;
     if (start + (uint32_t)datalen > flen) return c;
     c.src = base + start;
@@ -170,7 +167,7 @@ struct WaveCopy {
     uint64_t dst[64];   // destination byte offset in the arena,
     uint32_t start[64]; // first destination chunk within the batch's run,
     uint32_t len[64];   // bytes
-    uint32_t head[64 * kMaxU];
+    uint32_t head[64 * kPgRounds];
 };
 
 template <bool NT>
@@ -238,74 +235,9 @@ __device__ __forceinline__ void issue_rounds(const PgArgs &a, WaveCopy &W, uint3
     __builtin_amdgcn_wave_barrier();  // head[] is rewritten by the next issue
 }
 
-template <int kU, bool NT>
-__device__ __forceinline__ void store_rounds(const PgArgs &a, const WaveCopy &W, int lane, const Round (&R)[kU])
-{
-    const int nl = lane == 63 ? 63 : lane + 1;
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-        const uint4 N0 = bperm16(R[u].A, nl);
-        const uint4 N = R[u].own ? R[u].E : N0;
-        if (R[u].act) {
-            const uint64_t s = W.src[R[u].p];
-            const uint32_t sh = (uint32_t)(s & 15u), L = W.len[R[u].p];
-            uint4 o = sh ? funnel16(R[u].A, N, sh) : R[u].A;
-            const int vb = (int)L - (int)(16u * R[u].k);
-            if (vb < 16) {
-                o.x = keep_bytes(o.x, vb);
-                o.y = keep_bytes(o.y, vb - 4);
-                o.z = keep_bytes(o.z, vb - 8);
-                o.w = keep_bytes(o.w, vb - 12);
-            }
-            stp<NT>(a.arena + W.dst[R[u].p] + 16u * R[u].k, o);
-        }
-    }
-}
-
-// The wave's 64 frames (lane = frame; L = 0: nothing to copy).  Software-pipelined: the
-// loads of the next kU rounds are issued before the current rounds are stored.
-template <int kU, bool NT>
-__device__ __forceinline__ void copy_batch(const PgArgs &a, WaveCopy &W, uint64_t src, uint64_t dst, uint32_t L,
-                                           int lane)
-{
-    const bool valid = L != 0u;
-    const unsigned long long vm = __ballot(valid);
-    if (vm == 0ull) return;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
-    const uint32_t nch = valid ? (L + 15u) >> 4 : 0u;
-    const uint32_t incl = wave_incl_scan(nch, lane);
-    const uint32_t start = incl - nch;
-    const uint32_t T = (uint32_t)__shfl(incl, 63, 64);
-    if (valid) {
-        W.src[rank] = src;
-        W.dst[rank] = dst;
-        W.start[rank] = start;
-        W.len[rank] = L;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
-    constexpr uint32_t kStep = 64u * kU;
-    Round X[kU], Y[kU];
-    issue_rounds<kU, NT>(a, W, 0u, T, valid, start, lane, le, X);
-    uint32_t r0 = 0;
-    for (;;) {
-        const bool more = r0 + kStep < T;
-        if (more) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, Y);
-        store_rounds<kU, NT>(a, W, lane, X);
-        if (!more) break;
-        r0 += kStep;
-        const bool more2 = r0 + kStep < T;
-        if (more2) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, X);
-        store_rounds<kU, NT>(a, W, lane, Y);
-        if (!more2) break;
-        r0 += kStep;
-    }
-    __builtin_amdgcn_wave_barrier();  // W is rewritten by the next batch
-}
-
-// store_rounds for copy_batch_pre: the workgroup's arena base is known only after the
-// look-back, so W.dst holds offsets relative to it; payloads past the arena capacity were
-// loaded but are not stored (they get no message either)
+// The stores of kU rounds: the workgroup's arena base is known only after the look-back, so
+// W.dst holds offsets relative to it; payloads past the arena capacity were loaded but are
+// not stored (they get no message either)
 template <int kU, bool NT>
 __device__ __forceinline__ void store_rounds_at(const PgArgs &a, const WaveCopy &W, int lane, const Round (&R)[kU],
                                                 uint64_t base)
@@ -333,11 +265,13 @@ __device__ __forceinline__ void store_rounds_at(const PgArgs &a, const WaveCopy 
     }
 }
 
-// copy_batch with the first kU rounds' loads issued before the workgroup's arena offset is
-// known: `finish` runs the look-back (and the workgroup barrier every wave must reach) while
-// those loads are in flight, and returns the workgroup's arena base.  `rel`: this lane's
-// payload offset relative to that base.
-template <int kU, bool NT, int PRE, typename F>
+// The wave's 64 frames (lane = frame; L = 0: nothing to copy), with the first two sets of kU
+// rounds' loads issued before the workgroup's arena offset is known: `finish` runs the
+// look-back (and the workgroup barrier every wave must reach) while those loads are in
+// flight, and returns the workgroup's arena base.  `rel`: this lane's payload offset relative
+// to that base.  Software-pipelined: the loads of the next kU rounds are issued before the
+// current rounds are stored.
+template <int kU, bool NT, typename F>
 __device__ __forceinline__ void copy_batch_pre(const PgArgs &a, WaveCopy &W, uint64_t src, uint64_t rel, uint32_t L,
                                                int lane, F finish)
 {
@@ -363,39 +297,22 @@ __device__ __forceinline__ void copy_batch_pre(const PgArgs &a, WaveCopy &W, uin
     constexpr uint32_t kStep = 64u * kU;
     Round X[kU], Y[kU];
     issue_rounds<kU, NT>(a, W, 0u, T, valid, start, lane, le, X);
-    if constexpr (PRE == 1) {
-        const uint64_t base = finish();
-        uint32_t r0 = 0;
-        for (;;) {
-            const bool more = r0 + kStep < T;
-            if (more) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, Y);
-            store_rounds_at<kU, NT>(a, W, lane, X, base);
-            if (!more) break;
-            r0 += kStep;
-            const bool more2 = r0 + kStep < T;
-            if (more2) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, X);
-            store_rounds_at<kU, NT>(a, W, lane, Y, base);
-            if (!more2) break;
-            r0 += kStep;
-        }
-    } else {
-        // both sets in flight across the look-back
-        bool haveY = kStep < T;
-        if (haveY) issue_rounds<kU, NT>(a, W, kStep, T, valid, start, lane, le, Y);
-        const uint64_t base = finish();
-        uint32_t r0 = 0;
-        for (;;) {
-            store_rounds_at<kU, NT>(a, W, lane, X, base);
-            if (!haveY) break;
-            r0 += kStep;
-            const bool more = r0 + kStep < T;
-            if (more) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, X);
-            store_rounds_at<kU, NT>(a, W, lane, Y, base);
-            if (!more) break;
-            r0 += kStep;
-            haveY = r0 + kStep < T;
-            if (haveY) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, Y);
-        }
+    // both sets in flight across the look-back
+    bool haveY = kStep < T;
+    if (haveY) issue_rounds<kU, NT>(a, W, kStep, T, valid, start, lane, le, Y);
+    const uint64_t base = finish();
+    uint32_t r0 = 0;
+    for (;;) {
+        store_rounds_at<kU, NT>(a, W, lane, X, base);
+        if (!haveY) break;
+        r0 += kStep;
+        const bool more = r0 + kStep < T;
+        if (more) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, X);
+        store_rounds_at<kU, NT>(a, W, lane, Y, base);
+        if (!more) break;
+        r0 += kStep;
+        haveY = r0 + kStep < T;
+        if (haveY) issue_rounds<kU, NT>(a, W, r0 + kStep, T, valid, start, lane, le, Y);
     }
     __builtin_amdgcn_wave_barrier();  // W is rewritten by the next batch
 }
@@ -460,130 +377,63 @@ __device__ __forceinline__ uint32_t look_back(const PgArgs &a, uint32_t vb, int 
     return excl;
 }
 
-// FPT frames per thread (workgroup = 256 * FPT frames, thread t owns frames FPT*t ..
-// FPT*t + FPT-1 for the scan; wave w copies frames [64 FPT w, 64 FPT (w+1)) 64 at a time).
-// TICKET: virtual workgroup ids from an atomic ticket (dispatch-order independent).
-template <int kU, bool NT, int FPT, bool TICKET, int PRE = 0, int TPB = kPgThreads, bool HDR = true>
-__global__ __launch_bounds__(TPB) void pg_gather(PgArgs a)
+// One thread per frame, kPgFrames frames per workgroup; virtual workgroup ids from an atomic
+// ticket (dispatch-order independent): the workgroup publishes its aggregate, issues its first
+// copy rounds, then wave 0 looks back while they are in flight.
+__global__ __launch_bounds__(kPgFrames) void pg_gather(PgArgs a)
 {
-    constexpr int FPB = TPB * FPT;
     __shared__ uint32_t s_vb, s_excl;
-    __shared__ uint32_t s_w[TPB / 64];
-    __shared__ WaveCopy s_wc[TPB / 64];
-    __shared__ uint64_t s_src[FPT > 1 ? FPB : 1];
-    __shared__ uint64_t s_dst[FPT > 1 ? FPB : 1];
-    __shared__ uint32_t s_len[FPT > 1 ? FPB : 1];
+    __shared__ uint32_t s_w[kPgFrames / 64];
+    __shared__ WaveCopy s_wc[kPgFrames / 64];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    uint32_t vb = blockIdx.x;
-    if constexpr (TICKET) {
-        if (t == 0) s_vb = (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base);
-        __syncthreads();
-        vb = s_vb;
-    }
-    const uint32_t i0 = vb * (uint32_t)FPB + (uint32_t)(t * FPT);
+    if (t == 0) s_vb = (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+    __syncthreads();
+    const uint32_t vb = s_vb;
+    const uint32_t i0 = vb * (uint32_t)kPgFrames + (uint32_t)t;
 
-    Cand c[FPT];
-    uint32_t mine = 0;
-#pragma unroll
-    for (int k = 0; k < FPT; ++k) {
-        c[k] = candidate<HDR>(a, i0 + k);
-        mine += (c[k].len + 15u) >> 4;
-    }
+    const Cand c = candidate(a, i0);
+    const uint32_t mine = (c.len + 15u) >> 4;
     const uint32_t incl = wave_incl_scan(mine, lane);
     if (lane == 63) s_w[w] = incl;
     __syncthreads();
     uint32_t agg = 0, wex = 0;
 #pragma unroll
-    for (int k = 0; k < TPB / 64; ++k) {
+    for (int k = 0; k < kPgFrames / 64; ++k) {
         agg += s_w[k];
         wex += k < w ? s_w[k] : 0u;
     }
-    if constexpr (PRE != 0 && FPT == 1) {
-        // publish the aggregate, issue the first copy rounds, then look back (wave 0) while
-        // they are in flight
-        if (w == 0 && lane == 0)
-            __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, vb ? kAgg : kIncl, agg),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t rel = ((uint64_t)wex + incl - mine) * 16ull;
-        auto finish = [&]() -> uint64_t {
-            if (w == 0) {
-                bool timed_out = false;
-                const uint32_t excl = vb ? look_back(a, vb, lane, timed_out) : 0u;
-                if (lane == 0) {
-                    if (vb)
-                        __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, kIncl, excl + agg),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (timed_out) atomicMax(a.used, ~0ull);
-                    else if (vb == a.nblocks - 1) atomicMax(a.used, (unsigned long long)(excl + agg) * 16ull);
-                    s_excl = excl;
-                }
+    if (w == 0 && lane == 0)
+        __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, vb ? kAgg : kIncl, agg),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t rel = ((uint64_t)wex + incl - mine) * 16ull;
+    auto finish = [&]() -> uint64_t {
+        if (w == 0) {
+            bool timed_out = false;
+            const uint32_t excl = vb ? look_back(a, vb, lane, timed_out) : 0u;
+            if (lane == 0) {
+                if (vb)
+                    __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, kIncl, excl + agg),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (timed_out) atomicMax(a.used, ~0ull);
+                else if (vb == a.nblocks - 1) atomicMax(a.used, (unsigned long long)(excl + agg) * 16ull);
+                s_excl = excl;
             }
-            __syncthreads();
-            const uint64_t base = (uint64_t)s_excl * 16ull;
-            const uint64_t off = base + rel;
-            const uint64_t r = 16ull * ((c[0].len + 15u) >> 4);
-            const bool fits = c[0].len != 0u && off + r <= a.arena_cap;
-            if (i0 < a.n) {
-                rxg_payload_msg m;
-                m.arena_off = fits ? off : 0ull;
-                m.len = fits ? c[0].len : 0u;
-                m.flags = fits ? c[0].flags : 0u;
-                a.msgs[i0] = m;
-            }
-            return base;
-        };
-        copy_batch_pre<kU, NT, PRE>(a, s_wc[w], c[0].src, rel, c[0].len, lane, finish);
-        return;
-    }
-    if (w == 0) {
-        if (lane == 0)
-            __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, vb ? kAgg : kIncl, agg),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool timed_out = false;
-        const uint32_t excl = vb ? look_back(a, vb, lane, timed_out) : 0u;
-        if (lane == 0) {
-            if (vb)
-                __hip_atomic_store((gu64 *)(a.status + vb), status_word(a.epoch, kIncl, excl + agg),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (timed_out) atomicMax(a.used, ~0ull);
-            else if (vb == a.nblocks - 1) atomicMax(a.used, (unsigned long long)(excl + agg) * 16ull);
-            s_excl = excl;
-        }
-    }
-    __syncthreads();
-    uint64_t off = ((uint64_t)s_excl + wex + incl - mine) * 16ull;
-    uint64_t dst[FPT];
-    uint32_t cl[FPT];
-#pragma unroll
-    for (int k = 0; k < FPT; ++k) {
-        const uint64_t r = 16ull * ((c[k].len + 15u) >> 4);
-        const bool fits = c[k].len != 0u && off + r <= a.arena_cap;
-        if (i0 + k < a.n) {
-            rxg_payload_msg m;
-            m.arena_off = fits ? off : 0ull;
-            m.len = fits ? c[k].len : 0u;
-            m.flags = fits ? c[k].flags : 0u;
-            a.msgs[i0 + k] = m;
-        }
-        dst[k] = off;
-        cl[k] = fits ? c[k].len : 0u;
-        off += r;
-    }
-    if constexpr (FPT == 1) {
-        copy_batch<kU, NT>(a, s_wc[w], c[0].src, dst[0], cl[0], lane);
-    } else {
-#pragma unroll
-        for (int k = 0; k < FPT; ++k) {
-            s_src[t * FPT + k] = c[k].src;
-            s_dst[t * FPT + k] = dst[k];
-            s_len[t * FPT + k] = cl[k];
         }
         __syncthreads();
-        for (int b = 0; b < FPT; ++b) {
-            const int q = w * 64 * FPT + b * 64 + lane;
-            copy_batch<kU, NT>(a, s_wc[w], s_src[q], s_dst[q], s_len[q], lane);
+        const uint64_t base = (uint64_t)s_excl * 16ull;
+        const uint64_t off = base + rel;
+        const uint64_t r = 16ull * ((c.len + 15u) >> 4);
+        const bool fits = c.len != 0u && off + r <= a.arena_cap;
+        if (i0 < a.n) {
+            rxg_payload_msg m;
+            m.arena_off = fits ? off : 0ull;
+            m.len = fits ? c.len : 0u;
+            m.flags = fits ? c.flags : 0u;
+            a.msgs[i0] = m;
         }
-    }
+        return base;
+    };
+    copy_batch_pre<kPgRounds, true>(a, s_wc[w], c.src, rel, c.len, lane, finish);
 }
 
 }  // namespace
@@ -611,10 +461,9 @@ hipError_t launch_payload(const LaunchPayload &P, hipStream_t st, uint32_t *laun
     *launched = 0;
     hipError_t e = hipMemsetAsync(P.used, 0, sizeof(unsigned long long), st);
     if (e != hipSuccess || P.n == 0) return e;
-    a.nblocks = (P.n + kPgThreadsProd - 1) / kPgThreadsProd;
-    const dim3 g(a.nblocks), b(kPgThreadsProd);
-    hipLaunchKernelGGL((pg_gather<kPgRoundsProd, true, 1, true, 2, kPgThreadsProd>), g, b, 0, st, a);
-    *launched = a.ticket ? a.nblocks : 0u;
+    a.nblocks = (P.n + kPgFrames - 1) / kPgFrames;
+    hipLaunchKernelGGL(pg_gather, dim3(a.nblocks), dim3(kPgFrames), 0, st, a);
+    *launched = a.nblocks;
     return hipGetLastError();
 }
 

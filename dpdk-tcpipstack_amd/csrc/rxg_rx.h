@@ -1,6 +1,5 @@
-// rxg_rx.h — the device code of the receive-path kernels (gfx950), shared by the product
-// kernels (rxg_kernels.hip) and the ablation kernels of the experiment library
-// (rxg_kernels_exp.hip, librxg_exp.so only).
+// rxg_rx.h — the device code of the receive-path kernels (gfx950), instantiated by
+// rxg_kernels.hip.
 //
 // One fused kernel body replaces, for a whole batch, the reference's per-packet
 //   ether_in (etherin.c:12-37) -> ip_in (ip.c:19-42) -> tcp_in (tcp_in.c:32-84)
@@ -409,7 +408,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     // share them: slice j (j < ck, the slices) is led by wave j, which classifies it, and the
     // waves w >= ck help the slice w mod ck, each of the 4 / ck waves of a slice taking its
     // streaming-class rounds part, part + 4 / ck, ... (part = w / ck), parking the fields in the
-    // leader's scratch; the leader classifies after a workgroup barrier.
+    // leader's scratch; the leader classifies after a workgroup barrier (HISTORY.md §9.R4).
     // Slices of at least 8 frames: below that a class has too few rounds to share, and the
     // barrier would only wait for the idle waves.  Barriers: one slice -- each wave passes one
     // when the slice is not all small (the leader on its class path), none otherwise; two
@@ -561,7 +560,7 @@ __device__ __forceinline__ void rx_body(RxArgs a, uint32_t blk, uint32_t nblk)
     if constexpr (SRV) {
         // The server: each wave adds its own counts (lanes 0-15, one atomic instruction), with
         // no workgroup reduction and no 64-bit cross-lane sum -- a served burst is one wave's
-        // latency, and these were 0.75 us of it.  A lane's bytes fit 32 bits
+        // latency, and these were 0.75 us of it (HISTORY.md §9.R4).  A lane's bytes fit 32 bits
         // here (a request is at most 2^20 frames: <= 2^14 slices of one frame per lane).
         uint32_t b = (uint32_t)bytes;
         b += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x128, 0xF, 0xF, false);  // row_ror:8
@@ -609,8 +608,7 @@ __global__ __launch_bounds__(256, 1) void rx_kernel(RxArgs a)
 }
 
 // ------------------------------------------------------------------- launch helpers ---
-// The kernel arguments and grid of a launch (host side, shared by rxg_kernels.hip and the
-// experiment library's rxg_kernels_exp.hip).
+// The kernel arguments and grid of a launch (host side, rxg_kernels.hip).
 struct RxGrid {
     uint32_t blocks = 0;
     bool deep = false;  // two-deep all-small prefetch (kDeepSlicesPerWave)

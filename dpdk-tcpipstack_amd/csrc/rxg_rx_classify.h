@@ -214,7 +214,7 @@ __device__ __forceinline__ bool arp_known(const RxArgs &a, uint32_t ip, const ui
 // ~0.4 % of the lanes at 64 K flows, a quarter of the slices) walk on.  Launched kernels walk
 // one lane at a time by the whole wave through scalar loads (the round-2 per-lane vector loop
 // drained the next slice's frames: C4 74.6 -> 73.6 us, 64 B frames at 64 K flows 28.7 -> 27.5,
-// DESIGN.md §9.R3); the server walks per lane with vector loads (see sload_bucket).
+// HISTORY.md §9.R3); the server walks per lane with vector loads (see sload_bucket).
 template <bool VWALK>
 __device__ __forceinline__ uint32_t tuple_lookup(const RxArgs &a, const Probe &P, uint32_t ports, uint32_t dst_raw,
                                                  uint32_t src_host)

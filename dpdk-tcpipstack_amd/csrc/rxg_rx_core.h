@@ -124,7 +124,7 @@ __device__ __forceinline__ T *as_global(uint64_t v)
 // one compare + ballot popcount and its fields are v_readlane -- no memory access and no
 // scalar-load wait per lookup.  Single-burst launches (MULTI false) read burst 0 directly.
 // A wave takes the launch's slices s = wave, wave + nwaves, ...  (Cutting the last, partial
-// generation's slices into pieces spread over more waves measured slower)
+// generation's slices into pieces spread over more waves measured slower, HISTORY.md §9.R3.)
 
 // launches with at least this many slices per wave take the two-deep all-small pipeline
 constexpr uint32_t kDeepSlicesPerWave = 16;

@@ -368,7 +368,7 @@ __device__ __forceinline__ Fields fields_small(uint8_t *fp, uint32_t len, uint32
         // beyond data_len are never written.  Two 2-byte stores: rewriting a 64-byte frame's
         // whole line instead measured slower, C4 tx 101.4 against 94.5 us, 64 B frames 40.9
         // against 33.6 (the write bytes count); so did queueing the line writes to the
-        // wave's end.
+        // wave's end (HISTORY.md §9.R3).
         if (len > 25u) *reinterpret_cast<uint16_t *>(fp + 24) = (uint16_t)bswap16(ip_ck);
         else if (len > 24u) fp[24] = (uint8_t)(ip_ck >> 8);
         if (len > 51u) *reinterpret_cast<uint16_t *>(fp + 50) = (uint16_t)bswap16(tcp_ck);
@@ -531,7 +531,7 @@ __device__ __forceinline__ Fields frame_round_compute(const RxArgs &a, uint32_t 
         // these classes are longer than 64 bytes: the group writes the frame's whole first
         // 64-byte line (chunks 0-3, as loaded, with the two checksum fields set) rather
         // than two 2-byte stores, so HBM sees full-line writes, not partial-line ones
-        // (C3 tx 327 -> 310 us).  Measured slower: holding the writes until
+        // (C3 tx 327 -> 310 us).  Measured slower (HISTORY.md §9): holding the writes until
         // the next round's loads are issued (322), non-temporal line stores, the whole
         // 128-byte L2 line, only the two 16-byte chunks holding the fields, the line writes
         // queued to the wave's end.

@@ -7,7 +7,7 @@
  *
  *   served_latency FRAME_BYTES BURST ITERS [PEERS] [BLOCKS]
  * Frames: Eth/IPv4/TCP ACKs with valid checksums to 192.168.78.2:80 from PEERS established
- * flows (default 1: the one-peer case of DESIGN.md §6.R3a); the TCB table holds the listener
+ * flows (default 1: the one-peer case of HISTORY.md §6.R3a); the TCB table holds the listener
  * and those flows.  Prints one JSON line: median / p10 / p90 microseconds per burst.
  */
 #include <stdint.h>

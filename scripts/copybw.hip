@@ -1,4 +1,4 @@
-// Copy ceilings for the payload gather: a hand-written 16-byte-per-lane copy,
+// Copy ceilings for the payload gather (HISTORY.md §9): a hand-written 16-byte-per-lane copy,
 // grid-stride over a persistent grid, 1.53 GB -> 1.53 GB.
 //   flat:  contiguous source
 //   rows:  2^20 rows of 1 456 B at a 1 536 B stride (C3's payload spans, 16-byte aligned;
@@ -7,7 +7,7 @@
 //          written to the same slot of a second pool -- the fused copy hand-off's traffic with
 //          whole-line writes, WL = 24 as shipped (the payload at its pool offset: header line
 //          and slot tail written) against WL = 23 (a 1 446 B payload from its first byte at the
-//          slot's start: DESIGN.md §4.F's line-aligned estimate)
+//          slot's start: DESIGN.md §5.F's line-aligned estimate)
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/copybw scripts/copybw.hip
 // Run:   build/copybw [workgroups per CU ...]   (default 2 4 8)
 #include <hip/hip_runtime.h>

@@ -3,7 +3,7 @@
 the reference's own hot-path files on: 1 500 B frames, 1 000 flows from 1 000 source IPs, +verify,
 after one pass has taught the ARP list every source.  Run in the survey's container class (no
 GPU needed), it gives the port / reference factor bench.py states beside its CPU baseline
-(DESIGN.md §6.R5).  Prints one JSON line.
+(HISTORY.md §6.R5).  Prints one JSON line.
   python scripts/cpu_calib.py [--seconds 5] [--frames 20000]"""
 import argparse
 import json

@@ -36,7 +36,7 @@ import bench  # noqa: E402  (its CPU-baseline leg times the reference path)
 import rxg  # noqa: E402
 
 BURSTS = [32, 256, 4096, 65536]
-# the served bursts, finer around the one-peer crossover
+# the served bursts, finer around the one-peer crossover (HISTORY.md §6.R3a)
 SRV_BURSTS = [32, 64, 96, 128, 160, 192, 256, 4096]
 SIZES = [64, 1500]
 FLOWS = [1, 1000, 65536]

@@ -1,4 +1,4 @@
-// readbw_rot.hip — read ceiling for the headline's access pattern: a
+// readbw_rot.hip — read ceiling for the headline's access pattern (HISTORY.md §6.R5): a
 // hand-written 16-byte-per-lane streaming read of two rotating 1.5 GiB buffers (as bench.py rotates its two C3
 // batches, so no launch re-reads the last one's tail from the 256 MB MALL), each thread
 // folding what it read into one word (4 B written per thread).  Grid-stride over a grid of

@@ -1,4 +1,4 @@
-// Micro-benchmark for a two-pass tx checksum generate: how long do the
+// Micro-benchmark for a two-pass tx checksum generate (HISTORY.md §9.R4): how long do the
 // checksum field writes alone take when they are NOT interleaved with the frame read stream?
 // Frames at a 1 536-byte stride (the C3 layout), 2^20 of them; per frame:
 //   v0  two 2-byte stores (bytes 24-25, 50-51) from a 4-byte-per-frame checksum array

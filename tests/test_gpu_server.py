@@ -347,7 +347,7 @@ def test_server_overflow_walks_see_mirror_writes(flags):
 
 @pytest.mark.parametrize("flags", PLACEMENTS)
 def test_server_small_bursts_of_every_size_class(srv_engine, flags):
-    """Round 4's server forms for a request of one slice: descriptors
+    """Round 4's server forms for a request of one slice (HISTORY.md §9.R4): descriptors
     carried in the mailbox (host bursts of <= 32 frames), the all-small path for a partial
     slice of small frames, and the workgroup's four waves sharing the streaming-class rounds
     of a slice of >= 8 frames.  Bursts of 1..64 frames holding every size class (small, 65-128,

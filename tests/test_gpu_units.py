@@ -1,4 +1,4 @@
-"""GPU parity over launch grids whose last generation of slices is partial (DESIGN.md §9,
+"""GPU parity over launch grids whose last generation of slices is partial (HISTORY.md §9,
 "Launch tail").
 
 A launch deals its slices round-robin over the waves of its grid (rxg_config.max_blocks caps
