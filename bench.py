@@ -33,24 +33,26 @@ import rxg  # noqa: E402  (after torch: one HIP runtime per process)
 METRIC = "Mpps + GB/s rx parse+checksum+classify, device-resident, 64B & 1500B frames"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Per-launch HBM traffic from the committed rocprofv3 PMC passes of this same command
-# (scripts/gpu_check.sh pmc; scripts/pmc_traffic.py applies the gfx950 FETCH_SIZE x2 fix).
-TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r02/c3/traffic.json",
-                 ("c2_64B_1flow", 1 << 20, 16): "profiles/r02/c2/traffic.json",
-                 ("c4_imix_64Kflows", 1 << 20, 16): "profiles/r02/c4/traffic.json",
-                 ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r02/c2multi/traffic.json",
-                 # the record-8 legs re-profiled on this tree (REC=8 scripts/gpu_prof.sh, scripts/runs/r05/r05o.sh)
-                 ("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r05/c3/traffic.json",
-                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r05/c2/traffic.json",
-                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r05/c4/traffic.json",
-                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r05/c2multi/traffic.json",
-                 # the 8(f) kernels over the headline's C3 batch (REC=8 scripts/gpu_prof.sh r05a tx3 pg3, this tree)
-                 ("tx_generate_dev", 1 << 20, 8): "profiles/r05/tx3/traffic.json",
-                 ("payload_gather", 1 << 20, 8): "profiles/r05/pg3/traffic.json",
-                 ("c3_rx_payload_fused", 1 << 20, 8): "profiles/r05/pf3/traffic.json",
-                 ("c3_rx_payload_by_reference", 1 << 20, 8): "profiles/r05/pr3/traffic.json",
-                 # the fixed-stride forms (rxg_rx_bursts_strided_dev), scripts/gpu_prof.sh c2s c2multis
-                 ("c2_64B_1flow_strided", 1 << 20, 8): "profiles/r05/c2s/traffic.json",
-                 ("c2_64B_1flow_multiburst_strided", 1 << 20, 8): "profiles/r05/c2multis/traffic.json"}
+# (scripts/gpu_prof.sh; scripts/pmc_traffic.py applies the gfx950 FETCH_SIZE x2 fix and stamps
+# the src= hash of the build the counted runs loaded: traffic_provenance).  All of round 6's
+# tree: REC=8 scripts/gpu_prof.sh ... c3 c2 c2s c4 c2multi c2multis pf3 pr3 tx3 pg3, and
+# REC=16 ... c3 c2 c4 c2multi.
+TRAFFIC_FILES = {("c3_1500B_1Kflows", 1 << 20, 8): "profiles/r06/c3/traffic.json",
+                 ("c2_64B_1flow", 1 << 20, 8): "profiles/r06/c2/traffic.json",
+                 ("c4_imix_64Kflows", 1 << 20, 8): "profiles/r06/c4/traffic.json",
+                 ("c2_64B_1flow_multiburst", 1 << 20, 8): "profiles/r06/c2multi/traffic.json",
+                 ("c2_64B_1flow_strided", 1 << 20, 8): "profiles/r06/c2s/traffic.json",
+                 ("c2_64B_1flow_multiburst_strided", 1 << 20, 8): "profiles/r06/c2multis/traffic.json",
+                 # the 8(f) kernels over the headline's C3 batch
+                 ("tx_generate_dev", 1 << 20, 8): "profiles/r06/tx3/traffic.json",
+                 ("payload_gather", 1 << 20, 8): "profiles/r06/pg3/traffic.json",
+                 ("c3_rx_payload_fused", 1 << 20, 8): "profiles/r06/pf3/traffic.json",
+                 ("c3_rx_payload_by_reference", 1 << 20, 8): "profiles/r06/pr3/traffic.json",
+                 # 16-byte records (bench.py --rec 16, and the legs' *_rec16 keys)
+                 ("c3_1500B_1Kflows", 1 << 20, 16): "profiles/r06/rec16/c3/traffic.json",
+                 ("c2_64B_1flow", 1 << 20, 16): "profiles/r06/rec16/c2/traffic.json",
+                 ("c4_imix_64Kflows", 1 << 20, 16): "profiles/r06/rec16/c4/traffic.json",
+                 ("c2_64B_1flow_multiburst", 1 << 20, 16): "profiles/r06/rec16/c2multi/traffic.json"}
 
 
 def traffic_of(name, n, rec):
@@ -997,6 +999,9 @@ def main():
     traffic, traffic_src = traffic_of(args.workload, wl.n, args.rec)
     prov = rxg.build_provenance()
     tprov = traffic_provenance(traffic_src, prov["build"])
+    # every traffic file the line's legs cite, against the same build
+    leg_files = sorted({tf for (_, _, r), tf in TRAFFIC_FILES.items() if r == args.rec})
+    stale = [tf for tf in leg_files if not traffic_provenance(tf, prov["build"])["traffic_matches_build"]]
 
     if rank == 0:
         line = {
@@ -1033,6 +1038,7 @@ def main():
                          # the traffic file's counted build against the library measured here
                          "traffic_src": tprov["traffic_src"],
                          "traffic_matches_build": tprov["traffic_matches_build"],
+                         "leg_traffic_files": len(leg_files), "leg_traffic_files_stale": stale,
                          "kernel_us": round(k_max_s * 1e6, 2),
                          "kernel_us_per_launch_pairs_rank0_median": round(k_med_s * 1e6, 2),
                          "kernel_us_min_over_ranks": round(k_min_s * 1e6, 2),
