@@ -962,6 +962,9 @@ extern "C" int rxg_counters_read(rxg_ctx *c, uint64_t *out)
     if (!c || !out) return fail(-EINVAL, "rxg_counters_read: NULL argument");
     if (int rc = set_device(c)) return rc;
     if (int rc = flush_delta(c)) return rc;
+    // bursts on caller streams add to the block too: every one launched so far is waited for
+    // (the table readers' events, sync_table_readers), then the context's stream
+    if (int rc = sync_table_readers(c)) return rc;
     HIP_OK(hipStreamSynchronize(c->stream));
     std::vector<uint64_t> rows((size_t)RXG_COUNTER_ROWS * RXG_NCOUNTERS);
     HIP_OK(hipMemcpyAsync(rows.data(), c->counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));

@@ -477,7 +477,8 @@ int rxg_tx_cksum_dev(rxg_ctx *ctx, const rxg_dev_tx_batch *b, void *stream);
 /* Counters                                                                   */
 /* ------------------------------------------------------------------------- */
 int rxg_counters_reset(rxg_ctx *ctx, void *stream);
-/* Synchronous read of the RXG_NCOUNTERS uint64 counters (the replica rows summed). */
+/* Synchronous read of the RXG_NCOUNTERS uint64 counters (the replica rows summed), after
+   every burst of this context has finished, on whatever stream it was launched. */
 int rxg_counters_read(rxg_ctx *ctx, uint64_t *out);
 /* The device keeps RXG_COUNTER_ROWS rows of the counter block: 64 replicas the kernels add
    into (so that workgroups do not all add to one cache line) and one row of corrections

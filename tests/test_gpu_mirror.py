@@ -410,3 +410,40 @@ def test_carried_list_then_an_overflowing_arp_list(reader, narp):
             if isinstance(v, rxg.DevArray):
                 v.free()
         eng.close()
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_counters_read_waits_for_caller_stream_bursts(lazy):
+    """rxg_counters_read is synchronous for every burst of the context, on whatever stream it
+    was launched (include/rxg.h): long bursts on two caller streams, then at once a read with
+    no synchronisation by the caller -- it counts every frame of both (the counter block is
+    the reference's tcp_in counters, tcp_in.c:18-19, merged per context)."""
+    engine = rxg.Engine(device=0, flags=rxg.CFG_STREAMS_OUTLIVE_WRITES if lazy else 0)
+    n, nflows = 1 << 20, 1000
+    dev = engine.synth(n=n, nflows=nflows, len_a=1500, seed=707, with_flows=True)
+    t0, l0 = rxg.synthetic_tcb_table(nflows)
+    out1, out2 = engine.alloc(n * 8), engine.alloc(n * 8)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for st in (s1, s2):
+        engine.stream_register(st.cuda_stream)
+    try:
+        engine.tcb_load(t0, l0)
+        engine.tcb_sync()
+        engine.sync()
+        for rnd in range(3):
+            engine.counters_reset()
+            engine.sync()
+            torch.cuda.synchronize()
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out1.ptr, 8, s1.cuda_stream)
+            engine.rx_burst_dev(dev["arena"].ptr, dev["off64"].ptr, dev["len"].ptr, n, out2.ptr, 8, s2.cuda_stream)
+            cnt = dict(zip(rxg.COUNTERS, engine.counters().tolist()))
+            assert cnt["rx"] == 2 * n and cnt["dispatch"] == 2 * n and cnt["tcb_hit_exact"] == 2 * n, (rnd, cnt)
+            assert cnt["bytes"] == 2 * n * 1500
+        torch.cuda.synchronize()
+    finally:
+        for d in (out1, out2):
+            d.free()
+        for v in dev.values():
+            if isinstance(v, rxg.DevArray):
+                v.free()
+        engine.close()
