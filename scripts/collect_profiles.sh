@@ -2,11 +2,11 @@
 # Copy scripts/gpu_final.sh's outputs (gpurun_out/$TAG) into the tracked profiles/$TAG:
 # the stamped PMC + trace directories per leg (REC 8 at the top, REC 16 under rec16/), the
 # bench command's rocprofv3 stats with its line, the GPU suite and smoke logs, the bench line.
-#   bash scripts/collect_profiles.sh r06
+#   bash scripts/collect_profiles.sh RUN_TAG [PROFILE_TAG]     (e.g. r06b r06)
 set -eu
-TAG=${1:?usage: collect_profiles.sh TAG}
+TAG=${1:?usage: collect_profiles.sh RUN_TAG [PROFILE_TAG]}
 SRC=gpurun_out/$TAG
-DST=profiles/$TAG
+DST=profiles/${2:-$TAG}
 mkdir -p "$DST/rec16" "$DST/bench_cmd" "$DST/check"
 for w in c3 c2 c2s c4 c2multi c2multis pf3 pr3 tx3 pg3; do rm -rf "$DST/$w"; cp -r "$SRC/p8/prof/$w" "$DST/"; done
 for w in c3 c2 c4 c2multi; do rm -rf "$DST/rec16/$w"; cp -r "$SRC/p16/prof/$w" "$DST/rec16/"; done
