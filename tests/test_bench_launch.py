@@ -107,3 +107,35 @@ def test_traffic_provenance_reports_a_mismatched_build(tmp_path):
     assert pmc_traffic.stamp([str(a), str(a)]) == {"build": built, "source_hash": "0123456789abcdef"}
     with pytest.raises(ValueError):
         pmc_traffic.stamp([str(a), str(b)])
+
+
+def test_cpu_baseline_host_and_replicas(monkeypatch):
+    """the CPU baseline states its host (model, nproc, affinity, quota) and
+    runs one replica per usable core, each after learning the WHOLE sample's sources, so every
+    replica walks the same ARP list as the 1-core leg (ip.c:26-32, arp.c:263-280)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bench
+    import oracle
+    import pktgen
+    import rxg
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    h = bench.host_cpus()
+    assert h["nproc"] >= 1 and h["affinity"] >= 1 and h["model"] is not None
+    if h["cgroup_quota_cpus"] is None:
+        assert h["usable"] == min(3, h["affinity"]) and "OMP_NUM_THREADS" in h["usable_from"]
+    else:
+        assert h["usable"] <= max(1, int(h["cgroup_quota_cpus"]))
+    # 40 sources spread over 400 frames: a replica's own quarter of the range holds only part
+    # of them, the whole sample all 40
+    nflows = 40
+    frames = [pktgen.frame(src_ip=pktgen.ip4(10, 1, 0, f), dst_ip=pktgen.ip4(192, 168, 78, 2), sport=1024 + f,
+                           dport=80, flags=0x10, payload=bytes(100)) for f in [i // 10 for i in range(400)]]
+    arena, off, lens = pktgen.pack_arena(frames)
+    tcb, live = rxg.synthetic_tcb_table(nflows)
+    oracle.arp_reset()
+    oracle.rx_batch(arena, off, lens, tcb, live, faithful=True, opt="O0")
+    assert oracle.arp_count("O0") == nflows
+    oracle.arp_reset()
+    r = bench.cpu_replicas(arena, off, lens, tcb, live, 4, 0.3)
+    assert r is not None and r["cores"] == 4 and r["arp_entries"] == nflows and r["mpps"] > 0
