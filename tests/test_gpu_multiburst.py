@@ -210,3 +210,59 @@ def test_multi_burst_gather_follows_the_replay_cursor(engine, kind):
     finally:
         for d in dev + [d_arena]:
             d.free()
+
+
+@pytest.mark.parametrize("kind", [rxg.REC8, rxg.REC48])
+def test_carried_patches_reach_every_launch_of_a_multi_burst_call(kind):
+    """tcbs[] writes made just before a call of more bursts than one launch takes (40 >
+    kMaxBursts = 32): the call's first launch carries the patch list and the
+    second, queued behind it on the context's stream, must classify against the patched table
+    too.  Every burst's records and the counters equal the oracle over the table after the
+    writes (remove_tcb tcp_tcb.c:175-186, state changes, a re-tupled slot)."""
+    # a fresh context: no table reader pending on another stream, so the list is carried
+    engine = rxg.Engine(device=0)
+    rng = random.Random(808)
+    rows, frames = pktgen.parity_set(seed=808, n=6000)
+    tcb, live = pktgen.table_arrays(rows)
+    engine.tcb_load(tcb, live)
+    engine.tcb_sync()
+    engine.sync()
+    live = live.copy()
+    tcb = tcb.copy()
+    for i in rng.sample([x for x in range(1, len(tcb)) if live[x]], 12):  # a short list: carried
+        if rng.random() < 0.5:
+            live[i] = 0
+            engine.tcb_remove(i)
+        else:
+            st = rng.choice([rxg.LISTENING, rxg.TCP_ESTABLISHED, rxg.SYN_RECV])
+            tcb["state"][i] = st
+            engine.tcb_set_state(i, st)
+    n, k = len(frames), 40
+    cuts = _cuts(rng, n, k)
+    order = list(range(n))
+    rng.shuffle(order)
+    arena, off = _pool(frames, order)
+    lens = np.array([len(f) for f in frames], dtype=np.uint16)
+    d_arena = engine.to_device(arena)
+    dev, bursts = [], []
+    try:
+        for j in range(k):
+            a, b = cuts[j], cuts[j + 1]
+            do, dl, dout = engine.to_device(off[a:b]), engine.to_device(lens[a:b]), engine.alloc((b - a) * kind)
+            dev += [do, dl, dout]
+            bursts.append((do.ptr, dl.ptr, b - a, dout.ptr))
+        engine.counters_reset()
+        engine.sync()
+        engine.rx_bursts_dev(d_arena.ptr, bursts, kind)
+        engine.sync()
+        got = np.concatenate([dev[3 * j + 2].download(rxg.rec_dtype(kind), cuts[j + 1] - cuts[j]) for j in range(k)])
+        parr, poff, plens = pktgen.pack_arena(frames)
+        exp, ecnt = oracle.rx_batch(parr, poff, plens, tcb, live)
+        if kind == rxg.REC8:
+            exp = rxg.rec8_pack(exp["c"])
+        assert got.tobytes() == exp.tobytes()
+        assert engine.counters().tolist() == ecnt.tolist()
+    finally:
+        for d in dev + [d_arena]:
+            d.free()
+        engine.close()
