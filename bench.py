@@ -2,16 +2,18 @@
 """bench.py — device-resident rx parse + checksum + classify throughput on MI355X.
 
 Workload (BASELINE.json configs[2], "C3"): 2^20 x 1500 B synthetic Eth/IPv4/TCP frames per
-GPU, 1 000 flows + 1 listener, records of 16 B, inputs resident in HBM before timing.  One
-step = one rxg_rx_burst_dev over the whole batch.  A 64 B leg (configs[1], "C2") is reported
-beside it with a rotating 1 GiB working set (16 copies of 2^20 frames) so the 256 MiB
-Infinity Cache cannot hold it.
+GPU, 1 000 flows + 1 listener, 8-byte records (--rec 16 for the other kind), two rotating
+1.5 GiB batches, inputs resident in HBM before timing.  One step = one rxg_rx_burst_dev over the
+whole batch.  Legs beside it: C2 64 B frames with a rotating 1 GiB working set
+(16 copies of 2^20 frames) so the 256 MiB Infinity Cache cannot hold it, C4 IMIX, the fused
+payload hand-off, tx generate, copy-inclusive C3 / C5, burst + replay under churn, small-burst
+latency; the CPU baseline at N = 1.
 
 Multi-GPU: one process per GPU (torch.distributed.run), weak scaling, every rank its own
 shard (seed + rank) and a replica of the TCB mirror; no data-path collective.  The only
 collective is the RCCL all-reduce that merges the per-GPU counters.
 
-Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+Prints ONE JSON line on rank 0 (DESIGN.md §6 for every field).
 """
 import argparse
 import json
